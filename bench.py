@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: ISTA (block best-response) iterations/s on dense fp32 A, 1..8 MI355X.
+
+One "step" = one iteration of the hot path (reference lasso.py:102-157): a
+full pass over the active block of A for A^T r, the shrink, a second pass for
+A D, the line search and the update -- all on the device, inputs resident in
+HBM before the timed region.
+
+  N = 1 : BASELINE configs[1]  m=8192 n=65536 fp32 A, one feature block.
+  N > 1 : BASELINE configs[2]  m=8192 n=65536*N, every GPU holds an 8192 x 65536
+          column shard (weak scaling; the per-GPU work of N = 1), one RCCL
+          all-reduce of m + 2 + N fp64 values per iteration.  The work unit is
+          one "block-iteration" = one iteration over an 8192 x 65536 fp32 block
+          (4.30e9 algorithmic bytes), so value = N x global iterations/s.
+          A strong-scaling measurement (the fixed 8192 x 65536 matrix split
+          N ways) is reported beside it under "strong".
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+M, N_PER_GPU = 8192, 65536
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "ISTA iters/sec on dense A (8192×65536 fp32) at 1/2/4/8 MI355X; HBM-roofline %"
+
+
+def alg_bytes_iter(m, w, sa=4, sv=8, k=1):
+    """two passes over the active block + vector I/O."""
+    return 2 * m * w * sa + sv * k * (5 * w + 5 * m)
+
+
+def alg_bytes_colpass(m, w, sa=4):
+    """k_colpass per launch: read A_b (m x w), r (m fp64), write g-partials once (w fp64)."""
+    return m * w * sa + 8 * m + 8 * w
+
+
+def alg_bytes_rowpass(m, w, sa=4):
+    """k_rowpass per launch: read A_b (m x w), D (w fp64), write s23 once (m fp64)."""
+    return m * w * sa + 8 * w + 8 * m
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--m", type=int, default=M)
+    ap.add_argument("--n-per-gpu", type=int, default=N_PER_GPU)
+    ap.add_argument("--block", type=int, default=1)
+    ap.add_argument("--type", default="float", choices=["float", "double", "bf16"])
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling leg (N > 1)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--seed", type=int, default=20190325)
+    return ap.parse_args()
+
+
+class Ctx:
+    def __init__(self, world):
+        import torch
+        import torch.distributed as dist
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", str(world)))
+        self.local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.dist = dist
+        if self.world > 1:
+            dist.init_process_group("gloo")
+        torch.cuda.set_device(self.local)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, v):
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0])
+
+
+def build_problem(ctx, m, n_total, block, type_name, seed):
+    import torch
+    from convex_optimization_amd.distributed import RankComm, shard_bounds
+    from convex_optimization_amd.parameters import device_instance
+    comm = RankComm(ctx.rank, ctx.world) if ctx.world > 1 else None
+    col_range = None
+    if ctx.world > 1:
+        bounds = shard_bounds(n_total, block, ctx.rank, ctx.world)
+        idx = torch.cat([torch.arange(s, e) for s, e in bounds]).to(f"cuda:{ctx.local}")
+        col_range = idx
+    gc, b, mu, _ = device_instance(m, n_total, 0.4, block, TYPE=type_name, seed=seed, device=ctx.local,
+                                   comm=comm, col_range=col_range)
+    torch.cuda.synchronize()
+    return gc, b, mu
+
+
+def timed_window(ctx, gc, steps, graph):
+    """barrier + sync, `steps` iterations, sync + barrier; returns max-over-ranks seconds."""
+    import torch
+    gc.set_kernel_timing(not graph)
+    ctx.barrier()
+    torch.cuda.synchronize()
+    gc.stream.synchronize()
+    t0 = time.perf_counter()
+    gc.solver_step(steps)
+    gc.stream.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ctx.barrier()
+    return ctx.max(t1 - t0)
+
+
+def measure(ctx, args, m, n_total):
+    gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed)
+    # graph replay needs per-kernel events off; timing mode launches eagerly with
+    # HIP events around every kernel on the solver stream.
+    gc.solver_reset(b, mu, use_graph=True)
+    gc.solver_step(args.warmup)
+    gc.stream.synchronize()
+    el_graph = timed_window(ctx, gc, args.steps, graph=True)
+    st = gc.solver_status()
+    gc.solver_reset(b, mu, use_graph=False)
+    gc.solver_step(args.warmup)
+    gc.stream.synchronize()
+    el_ev = timed_window(ctx, gc, args.steps, graph=False)
+    times, samples = gc.kernel_times()
+    gc.set_kernel_timing(False)
+    return dict(gc=gc, el_graph=el_graph, el_events=el_ev, kernel_ms=times, samples=samples, status=st,
+                w_local=gc.MAT_WIDTH, b=b, mu=mu)
+
+
+def cpu_baseline(gc, b, mu, seconds):
+    """The oracle (C restatement of the reference iteration) on this host's cores,
+    bounded sample of the same workload: the same A (copied back to host fp32),
+    as many iterations as fit in about `seconds` of CPU time."""
+    import numpy as np
+    from oracle import oracle
+    oracle.build()
+    H, W = gc.MAT_HEIGHT, gc.MAT_WIDTH
+    A = gc.A_b_gpu.permute(1, 0, 2).reshape(H, gc.Block * W).cpu().numpy()
+    A = np.ascontiguousarray(A)
+    bh = b.cpu().numpy()
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    oracle.run(A, bh, mu, gc.Block, 2, nthreads=threads)
+    per = (time.perf_counter() - t0) / 2
+    iters = int(max(3, min(200, seconds / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    oracle.run(A, bh, mu, gc.Block, iters, nthreads=threads)
+    el = time.perf_counter() - t0
+    return {"value": iters / el, "unit": "iters/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/bpgl_oracle.c oracle_run, {iters} iterations from x=0 on the same "
+                      f"{H}x{gc.Block * W} fp32 A and b, {threads} OpenMP threads (fp64 arithmetic)"}
+
+
+def pmc_traffic(workload_key):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        data = json.load(open(path))
+        return data.get(workload_key)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    ctx = Ctx(args.gpus)
+    G = ctx.world
+    m = args.m
+    n_total = args.n_per_gpu * G
+    res = measure(ctx, args, m, n_total)
+    w = res["w_local"]
+    iters_s_graph = args.steps / res["el_graph"]
+    iters_s_ev = args.steps / res["el_events"]
+    kms = res["kernel_ms"]
+    dom = max(("colpass", "rowpass"), key=lambda k: kms[k])
+    sa = {"float": 4, "double": 8, "bf16": 2}[args.type]
+    dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(m, w, sa)
+    achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
+    workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}"
+    traffic = pmc_traffic(workload_key)
+    out = {
+        "metric": METRIC,
+        "value": iters_s_graph * G,
+        "unit": "block-iters/s (1 block-iter = 1 iteration over an 8192x65536 fp32 column block)"
+        if G > 1 else "iters/s",
+        "n_gpus": G,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": res["el_graph"] / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (A ~ N(0,1) rows unit-norm, generated in HBM; x_true density 0.4; b = A x_true + 0.01 e)",
+        "config": {
+            "workload": ("configs[1]: m=8192 n=65536 fp32 A, 1 feature block, 1 GPU" if G == 1 else
+                         f"configs[2]-style: m={m} n={n_total} fp32 A, 1 feature block, column-sharded "
+                         f"{w} cols/GPU x {G} GPUs, RCCL all-reduce per iteration"),
+            "m": m, "n": n_total, "n_local": w, "feature_blocks": args.block, "a_storage": args.type,
+            "accumulate": "fp64", "parallelism": f"column-shard x{G}",
+            "global_iters_per_s": iters_s_graph,
+            "alg_bytes_per_iter_per_gpu": alg_bytes_iter(m, w, sa),
+            "hbm_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(m, w, sa),
+            "iter_roofline_frac": iters_s_graph * alg_bytes_iter(m, w, sa) / (HBM_PEAK_GBS * 1e9),
+            "launch_mode": "hipGraph replay of one iteration (value); eager + HIP events (kernel times)",
+            "iters_per_s_eager_with_events": iters_s_ev,
+            "kernel_avg_ms": kms,
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": "k_colpass<float,0> (A^T r)" if dom == "colpass" else "k_rowpass<float> (A D)",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "alg_bytes_per_launch": dom_bytes,
+            "avg_launch_ms": kms[dom],
+        },
+    }
+    if G > 1 and not args.no_strong:
+        del res
+        torch.cuda.empty_cache()
+        a2 = argparse.Namespace(**vars(args))
+        strong = measure(ctx, a2, m, args.n_per_gpu)
+        out["strong"] = {"value": args.steps / strong["el_graph"], "unit": "iters/s",
+                         "config": f"m={m} n={args.n_per_gpu} split {G} ways ({strong['w_local']} cols/GPU)",
+                         "kernel_avg_ms": strong["kernel_ms"]}
+        res = strong
+    if G == 1 and ctx.rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds)
+    if ctx.rank == 0:
+        print(json.dumps(out))
+    if ctx.world > 1:
+        ctx.dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

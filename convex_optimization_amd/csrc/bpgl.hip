@@ -1,0 +1,547 @@
+// bpgl -- C ABI (include/bpgl.h) over the gfx950 kernels of bpgl_kernels.h.
+//
+// Host-side responsibilities: validate shapes before any launch, carve the
+// caller's scratch buffer, choose the launch geometry, enqueue the per-block
+// update sequence (optionally as one captured hipGraph per iteration), drive
+// the RCCL all-reduce of the column-sharded multi-GPU path, and time kernels
+// with HIP events when asked.  No hipMalloc anywhere: device memory belongs to
+// the caller (PyTorch).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bpgl.h"
+#include "bpgl_kernels.h"
+
+using namespace bpgl;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(BPGL_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+#define LAUNCH_CHECK(what)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ != hipSuccess) return fail(BPGL_E_HIP, "launch %s: %s", what, hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kTimedKinds = 7;
+constexpr int kMaxRanks = 64;
+
+int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
+int elem_bytes(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 8 : 2; }
+int64_t up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+}  // namespace
+
+struct bpgl_ctx {
+    int device = 0, dtype = BPGL_F32;
+    int64_t m = 0, n_local = 0, w = 0, wp = 0;
+    int32_t nblock = 1;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // geometry
+    int nseg = 0, nchunk = 0, R = 0, segw = 0, nparts = 0;
+    // bound buffers
+    const void* A = nullptr;
+    int64_t lda = 0, block_stride = 0;
+    bool bound = false, have_diag = false;
+    Params p{};
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1;
+    // solver
+    bool solver = false, use_graph = false;
+    hipGraphExec_t gexec = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> evs;   // (kinds + 1) events per timed iteration
+    int64_t timed_iters = 0;
+    double wall_tick_s = 1e-8;
+};
+
+namespace {
+
+void geometry(bpgl_ctx* c) {
+    const int V = vec_elems(c->dtype);
+    c->segw = 64 * V * kU;
+    c->wp = up(c->w, V);
+    c->nseg = (int)cdiv(c->wp, c->segw);
+    // ~8 blocks per CU on 256 CUs, rows per chunk a multiple of 16 (4 waves x 4 rows)
+    const int64_t target = 2048;
+    int64_t nchunk = std::max<int64_t>(1, cdiv(target, c->nseg));
+    nchunk = std::min<int64_t>(nchunk, cdiv(c->m, 16));
+    int64_t R = up(cdiv(c->m, nchunk), 16);
+    c->R = (int)R;
+    c->nchunk = (int)cdiv(c->m, R);
+    c->nparts = (int)cdiv(c->wp, kThreads);
+}
+
+struct Carve {
+    int64_t off = 0;
+    int64_t take(int64_t bytes) {
+        int64_t o = off;
+        off = up(off + bytes, 256);
+        return o;
+    }
+};
+
+// scratch layout (offsets in bytes)
+struct Layout {
+    int64_t slab_g, slab_s, g, D, parts, comm, r, Ax, st, diag, rec, total;
+};
+Layout layout(const bpgl_ctx* c) {
+    Carve k;
+    Layout L;
+    L.st = k.take(sizeof(DevState));
+    L.slab_g = k.take(8 * (int64_t)c->nchunk * c->wp);
+    L.slab_s = k.take(8 * (int64_t)c->nseg * c->m);
+    L.g = k.take(8 * c->wp);
+    L.D = k.take(8 * c->wp);
+    L.parts = k.take(8 * 4 * (int64_t)c->nparts);
+    L.comm = k.take(8 * (c->m + 2 + kMaxRanks));
+    L.r = k.take(8 * c->m);
+    L.Ax = k.take(8 * (int64_t)c->nblock * c->m);
+    L.diag = k.take(8 * (int64_t)c->nblock * c->wp);
+    L.rec = k.take(8 * (int64_t)c->nblock * c->wp);
+    L.total = k.off;
+    return L;
+}
+
+dim3 grid_tiles(const bpgl_ctx* c) { return dim3((unsigned)((int64_t)c->nseg * c->nchunk)); }
+
+template <typename T>
+int launch_colpass(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_block) {
+    if (mode == 0)
+        hipLaunchKernelGGL((k_colpass<T, 0>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+    else
+        hipLaunchKernelGGL((k_colpass<T, 1>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+    LAUNCH_CHECK("k_colpass");
+    return 0;
+}
+int colpass(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_block) {
+    switch (c->dtype) {
+        case BPGL_F32: return launch_colpass<float>(c, mode, vec, slab, fixed_block);
+        case BPGL_F64: return launch_colpass<double>(c, mode, vec, slab, fixed_block);
+        default: return launch_colpass<bf16_t>(c, mode, vec, slab, fixed_block);
+    }
+}
+template <typename T>
+int launch_rowpass(bpgl_ctx* c, const double* d, double* slab, int fixed_block) {
+    hipLaunchKernelGGL((k_rowpass<T>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, d, slab, fixed_block);
+    LAUNCH_CHECK("k_rowpass");
+    return 0;
+}
+int rowpass(bpgl_ctx* c, const double* d, double* slab, int fixed_block) {
+    switch (c->dtype) {
+        case BPGL_F32: return launch_rowpass<float>(c, d, slab, fixed_block);
+        case BPGL_F64: return launch_rowpass<double>(c, d, slab, fixed_block);
+        default: return launch_rowpass<bf16_t>(c, d, slab, fixed_block);
+    }
+}
+
+int rowreduce(bpgl_ctx* c, const double* slab, double* out, int solver) {
+    hipLaunchKernelGGL(k_rowreduce, dim3((unsigned)cdiv(c->m, kThreads)), dim3(kThreads), 0, c->stream,
+                       c->p, slab, out, solver);
+    LAUNCH_CHECK("k_rowreduce");
+    return 0;
+}
+
+int check_ready(const bpgl_ctx* c) {
+    if (!c) return fail(BPGL_E_ARG, "null context");
+    if (!c->bound) return fail(BPGL_E_STATE, "bpgl_bind has not been called");
+    return 0;
+}
+
+void ev_record(bpgl_ctx* c, int64_t it, int k) {
+    if (!c->timing) return;
+    const size_t idx = (size_t)it * (kTimedKinds + 1) + k;
+    while (c->evs.size() <= idx) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->evs.push_back(e);
+    }
+    hipEventRecord(c->evs[idx], c->stream);
+}
+
+// One block update, enqueued on c->stream.  The block index and every
+// iteration-dependent value are read on the device from the state words, so
+// the same launch sequence (or its captured graph) serves every iteration.
+int enqueue_iteration(bpgl_ctx* c, int64_t timed_it) {
+    int rc;
+    ev_record(c, timed_it, 0);
+    if ((rc = colpass(c, 0, c->p.r, c->p.slab_g, -1))) return rc;
+    ev_record(c, timed_it, 1);
+    hipLaunchKernelGGL(k_shrink, dim3((unsigned)c->nparts), dim3(kThreads), 0, c->stream, c->p);
+    LAUNCH_CHECK("k_shrink");
+    ev_record(c, timed_it, 2);
+    if ((rc = rowpass(c, c->p.D, c->p.slab_s, -1))) return rc;
+    ev_record(c, timed_it, 3);
+    if ((rc = rowreduce(c, c->p.slab_s, c->p.comm, 1))) return rc;
+    ev_record(c, timed_it, 4);
+    if (c->comm) {
+        ncclResult_t nr = ncclAllReduce(c->p.comm, c->p.comm, (size_t)(c->m + 2 + c->nranks), ncclFloat64,
+                                        ncclSum, c->comm, c->stream);
+        if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
+    }
+    ev_record(c, timed_it, 5);
+    hipLaunchKernelGGL(k_step, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
+    LAUNCH_CHECK("k_step");
+    ev_record(c, timed_it, 6);
+    const int64_t nupd = std::max<int64_t>(c->wp, c->m);
+    const unsigned ublocks = (unsigned)std::min<int64_t>(cdiv(nupd, kThreads), 1024);
+    hipLaunchKernelGGL(k_update, dim3(ublocks), dim3(kThreads), 0, c->stream, c->p);
+    LAUNCH_CHECK("k_update");
+    ev_record(c, timed_it, 7);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* bpgl_last_error(void) { return g_err.c_str(); }
+int bpgl_version(void) { return 100; }
+
+int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_local, int32_t nblock,
+                void* hip_stream) {
+    if (!out) return fail(BPGL_E_ARG, "out is null");
+    *out = nullptr;
+    if (a_dtype != BPGL_F32 && a_dtype != BPGL_F64 && a_dtype != BPGL_BF16)
+        return fail(BPGL_E_ARG, "unknown dtype %d", a_dtype);
+    if (m <= 0 || n_local <= 0 || nblock <= 0) return fail(BPGL_E_ARG, "m, n_local, nblock must be > 0");
+    if (n_local % nblock) return fail(BPGL_E_ARG, "n_local (%lld) must be divisible by nblock (%d)",
+                                      (long long)n_local, nblock);
+    if (m > (int64_t)1 << 40) return fail(BPGL_E_ARG, "m too large");
+    HIP_TRY(hipSetDevice(device));
+    bpgl_ctx* c = new bpgl_ctx();
+    c->device = device;
+    c->dtype = a_dtype;
+    c->m = m;
+    c->n_local = n_local;
+    c->nblock = nblock;
+    c->w = n_local / nblock;
+    if (hip_stream) {
+        c->stream = (hipStream_t)hip_stream;
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            return fail(BPGL_E_HIP, "hipStreamCreate failed");
+        }
+        c->own_stream = true;
+    }
+    int rate_khz = 0;
+    if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && rate_khz > 0)
+        c->wall_tick_s = 1.0 / (1000.0 * rate_khz);
+    geometry(c);
+    if (c->nchunk > 0x7fffffff / std::max(1, c->nseg)) {
+        delete c;
+        return fail(BPGL_E_ARG, "grid too large");
+    }
+    *out = c;
+    return 0;
+}
+
+void bpgl_destroy(bpgl_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->gexec) hipGraphExecDestroy(c->gexec);
+    for (auto e : c->evs) hipEventDestroy(e);
+    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->own_stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void* bpgl_stream(bpgl_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int64_t bpgl_scratch_bytes(const bpgl_ctx* c) { return c ? layout(c).total : -1; }
+int64_t bpgl_block_width_padded(const bpgl_ctx* c) { return c ? c->wp : -1; }
+
+int bpgl_geometry(const bpgl_ctx* c, int32_t* nseg, int32_t* nchunk, int32_t* R, int32_t* segw) {
+    if (!c) return fail(BPGL_E_ARG, "null context");
+    if (nseg) *nseg = c->nseg;
+    if (nchunk) *nchunk = c->nchunk;
+    if (R) *R = c->R;
+    if (segw) *segw = c->segw;
+    return 0;
+}
+
+int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, void* scratch,
+              int64_t scratch_bytes) {
+    if (!c) return fail(BPGL_E_ARG, "null context");
+    if (!A || !scratch) return fail(BPGL_E_ARG, "A and scratch must be non-null");
+    const int eb = elem_bytes(c->dtype), V = vec_elems(c->dtype);
+    if (((uintptr_t)A) % 16) return fail(BPGL_E_ARG, "A must be 16-byte aligned");
+    if (((uintptr_t)scratch) % 256) return fail(BPGL_E_ARG, "scratch must be 256-byte aligned");
+    if (lda < c->wp || lda % V) return fail(BPGL_E_ARG, "lda (%lld) must be >= w_pad (%lld) and a multiple of %d",
+                                            (long long)lda, (long long)c->wp, V);
+    if (c->nblock > 1 && (block_stride % V || block_stride < c->wp))
+        return fail(BPGL_E_ARG, "block_stride (%lld) must be a multiple of %d and >= w_pad",
+                    (long long)block_stride, V);
+    (void)eb;
+    const Layout L = layout(c);
+    if (scratch_bytes < L.total)
+        return fail(BPGL_E_SCRATCH, "scratch too small: %lld < %lld", (long long)scratch_bytes, (long long)L.total);
+    c->A = A;
+    c->lda = lda;
+    c->block_stride = block_stride;
+    char* s = (char*)scratch;
+    Params& p = c->p;
+    p = Params{};
+    p.A = A;
+    p.lda = lda;
+    p.block_stride = block_stride;
+    p.m = c->m;
+    p.w = c->w;
+    p.wp = c->wp;
+    p.nblock = c->nblock;
+    p.nseg = c->nseg;
+    p.nchunk = c->nchunk;
+    p.R = c->R;
+    p.nparts = c->nparts;
+    p.nranks = c->nranks;
+    p.rank = c->rank;
+    p.slab_g = (double*)(s + L.slab_g);
+    p.slab_s = (double*)(s + L.slab_s);
+    p.g = (double*)(s + L.g);
+    p.D = (double*)(s + L.D);
+    p.parts = (double*)(s + L.parts);
+    p.comm = (double*)(s + L.comm);
+    p.r = (double*)(s + L.r);
+    p.Ax = (double*)(s + L.Ax);
+    p.st = (DevState*)(s + L.st);
+    p.diag = (const double*)(s + L.diag);
+    p.rec = (const double*)(s + L.rec);
+    p.wall_tick_s = c->wall_tick_s;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemsetAsync(s + L.st, 0, sizeof(DevState), c->stream));
+    HIP_TRY(hipMemsetAsync(s + L.D, 0, 8 * c->wp, c->stream));
+    c->bound = true;
+    c->have_diag = false;
+    c->solver = false;
+    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    return 0;
+}
+
+int bpgl_diag_ata(bpgl_ctx* c, double* out) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    for (int b = 0; b < c->nblock; ++b) {
+        if ((rc = colpass(c, 1, nullptr, c->p.slab_g, b))) return rc;
+        double* dst = const_cast<double*>(c->p.diag) + (int64_t)b * c->wp;
+        double* rdst = const_cast<double*>(c->p.rec) + (int64_t)b * c->wp;
+        hipLaunchKernelGGL(k_colreduce, dim3((unsigned)cdiv(c->wp, kThreads)), dim3(kThreads), 0, c->stream,
+                           c->p.slab_g, c->wp, c->nchunk, dst, rdst);
+        LAUNCH_CHECK("k_colreduce");
+    }
+    if (out)
+        HIP_TRY(hipMemcpyAsync(out, c->p.diag, 8 * (size_t)c->nblock * c->wp, hipMemcpyDeviceToDevice, c->stream));
+    c->have_diag = true;
+    return 0;
+}
+
+int bpgl_mtv(bpgl_ctx* c, int32_t block, const double* r, double* g) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    if (block < 0 || block >= c->nblock) return fail(BPGL_E_ARG, "block %d out of range", block);
+    if (!r || !g) return fail(BPGL_E_ARG, "null vector");
+    HIP_TRY(hipSetDevice(c->device));
+    if ((rc = colpass(c, 0, r, c->p.slab_g, block))) return rc;
+    hipLaunchKernelGGL(k_colreduce, dim3((unsigned)cdiv(c->wp, kThreads)), dim3(kThreads), 0, c->stream,
+                       c->p.slab_g, c->wp, c->nchunk, g, (double*)nullptr);
+    LAUNCH_CHECK("k_colreduce");
+    return 0;
+}
+
+int bpgl_mv(bpgl_ctx* c, int32_t block, const double* d, double* s) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    if (block < 0 || block >= c->nblock) return fail(BPGL_E_ARG, "block %d out of range", block);
+    if (!d || !s) return fail(BPGL_E_ARG, "null vector");
+    HIP_TRY(hipSetDevice(c->device));
+    if ((rc = rowpass(c, d, c->p.slab_s, block))) return rc;
+    return rowreduce(c, c->p.slab_s, s, 0);
+}
+
+int bpgl_comm_unique_id(void* out128) {
+    if (!out128) return fail(BPGL_E_ARG, "null buffer");
+    ncclUniqueId id;
+    ncclResult_t nr = ncclGetUniqueId(&id);
+    if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclGetUniqueId: %s", ncclGetErrorString(nr));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    memcpy(out128, &id, 128);
+    return 0;
+}
+
+int bpgl_comm_init(bpgl_ctx* c, const void* uid, int rank, int nranks) {
+    if (!c || !uid) return fail(BPGL_E_ARG, "null argument");
+    if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
+        return fail(BPGL_E_ARG, "bad rank %d / nranks %d", rank, nranks);
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    c->rank = rank;
+    c->nranks = nranks;
+    c->p.rank = rank;
+    c->p.nranks = nranks;
+    if (nranks > 1) {
+        ncclUniqueId id;
+        memcpy(&id, uid, 128);
+        ncclResult_t nr = ncclCommInitRank(&c->comm, nranks, id, rank);
+        if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(nr));
+    }
+    c->p.has_comm = c->comm != nullptr;
+    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    return 0;
+}
+
+int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const int32_t* order,
+                      int64_t order_len, double err_bound, double* err_iter, double* time_iter,
+                      int64_t record_len, int use_graph) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    if (!c->have_diag) return fail(BPGL_E_STATE, "bpgl_diag_ata must run before the solver");
+    if (!b || !x) return fail(BPGL_E_ARG, "b and x must be non-null");
+    if (order && order_len <= 0) return fail(BPGL_E_ARG, "order_len must be > 0");
+    if (!(mu >= 0.0)) return fail(BPGL_E_ARG, "mu must be >= 0");
+    HIP_TRY(hipSetDevice(c->device));
+    Params& p = c->p;
+    p.b = b;
+    p.x = x;
+    p.mu = mu;
+    p.order = order;
+    p.order_len = order ? order_len : 0;
+    p.err_bound = err_bound;
+    p.err_iter = err_iter;
+    p.time_iter = time_iter;
+    p.rec_len = (err_iter || time_iter) ? record_len : 0;
+    // Ax_k = A_k x_k for the initial point (lasso.py:91 starts from 0)
+    for (int k = 0; k < c->nblock; ++k) {
+        if ((rc = rowpass(c, x + (int64_t)k * c->wp, p.slab_s, k))) return rc;
+        if ((rc = rowreduce(c, p.slab_s, p.Ax + (int64_t)k * c->m, 0))) return rc;
+    }
+    if (c->comm) {
+        // column-sharded ranks: every Ax_k is a sum over ranks
+        ncclResult_t nr = ncclAllReduce(p.Ax, p.Ax, (size_t)c->nblock * c->m, ncclFloat64, ncclSum, c->comm,
+                                        c->stream);
+        if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
+    }
+    hipLaunchKernelGGL(k_reset, dim3((unsigned)std::min<int64_t>(cdiv(c->m, kThreads), 1024)), dim3(kThreads), 0,
+                       c->stream, p);
+    LAUNCH_CHECK("k_reset");
+    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    c->use_graph = use_graph != 0;
+    if (c->use_graph) {
+        hipGraph_t graph = nullptr;
+        const bool was_timing = c->timing;
+        c->timing = false;
+        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        rc = enqueue_iteration(c, 0);
+        hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+        c->timing = was_timing;
+        if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
+        if (ec != hipSuccess) return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
+        hipError_t ei = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (ei != hipSuccess) return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+    }
+    c->solver = true;
+    c->timed_iters = 0;
+    return 0;
+}
+
+int bpgl_solver_step(bpgl_ctx* c, int64_t n_iter) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    if (!c->solver) return fail(BPGL_E_STATE, "bpgl_solver_reset has not been called");
+    if (n_iter < 0) return fail(BPGL_E_ARG, "n_iter < 0");
+    HIP_TRY(hipSetDevice(c->device));
+    for (int64_t i = 0; i < n_iter; ++i) {
+        if (c->timing || !c->gexec) {
+            if ((rc = enqueue_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
+            if (c->timing) c->timed_iters++;
+        } else {
+            HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
+        }
+    }
+    return 0;
+}
+
+int bpgl_solver_status(bpgl_ctx* c, int64_t* iters_done, int* stopped, int64_t* t_last, double* gamma,
+                       double* err) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    DevState st;
+    HIP_TRY(hipMemcpyAsync(&st, c->p.st, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (iters_done) *iters_done = st.iters;
+    if (stopped) *stopped = (int)st.done;
+    if (t_last) *t_last = st.t_last;
+    if (gamma) *gamma = st.gamma;
+    if (err) *err = st.err;
+    return 0;
+}
+
+const double* bpgl_solver_residual(bpgl_ctx* c) { return c ? c->p.r : nullptr; }
+
+int bpgl_iterate(bpgl_ctx* c, int64_t n_iter, const int32_t* order, double mu, const double* b, double* x,
+                 double* err_iter, double* time_iter, double err_bound, int64_t* iters_done) {
+    int rc;
+    if ((rc = bpgl_solver_reset(c, b, mu, x, order, order ? n_iter : 0, err_bound, err_iter, time_iter, n_iter,
+                                1)))
+        return rc;
+    if ((rc = bpgl_solver_step(c, n_iter))) return rc;
+    if (iters_done) return bpgl_solver_status(c, iters_done, nullptr, nullptr, nullptr, nullptr);
+    return 0;
+}
+
+int bpgl_set_kernel_timing(bpgl_ctx* c, int enable) {
+    if (!c) return fail(BPGL_E_ARG, "null context");
+    c->timing = enable != 0;
+    c->timed_iters = 0;
+    return 0;
+}
+
+int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
+    if (!c || !avg_ms) return fail(BPGL_E_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // kinds: 0 colpass, 1 shrink, 2 rowpass, 3 rowreduce, 4 allreduce, 5 step, 6 update
+    double sum[kTimedKinds] = {0};
+    for (int64_t it = 0; it < c->timed_iters; ++it) {
+        for (int k = 0; k < kTimedKinds; ++k) {
+            float ms = 0.f;
+            const size_t i0 = (size_t)it * (kTimedKinds + 1) + k;
+            HIP_TRY(hipEventElapsedTime(&ms, c->evs[i0], c->evs[i0 + 1]));
+            sum[k] += ms;
+        }
+    }
+    for (int k = 0; k < kTimedKinds; ++k) avg_ms[k] = c->timed_iters ? sum[k] / c->timed_iters : 0.0;
+    if (samples) *samples = c->timed_iters;
+    c->timed_iters = 0;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,499 @@
+// bpgl device kernels (gfx950 / CDNA4).  Included by bpgl.hip only.
+//
+// Hot path of one block update (reference lasso.py:102-157):
+//   k_colpass   partial  g = A_b^T r  over a (row chunk x column segment) tile,
+//               fp64 accumulation, cross-wave LDS reduction, one fp64 slab row
+//               per row chunk (replaces K1 mul_mat_t_vec_diffsize,
+//               gpu_calculation.py:20-55, whose partials were summed on the host)
+//   k_shrink    fixed-order split-K sum of the slab, s14/s15 best response,
+//               direction D, l1 norms and the error criterion
+//               (lasso.py:114-119, cpu_calculation.py:5-20)
+//   k_rowpass   partial  s23 = A_b D  per (row, column segment), wave-level
+//               transposed butterfly reduction (replaces K2 mul_mat_vec_diffsize,
+//               gpu_calculation.py:58-91, whose lanes were strided by a row)
+//   k_rowreduce fixed-order sum over column segments + l1/err partials into
+//               the all-reduce buffer
+//   k_step      exact line search and stopping rule (lasso.py:129-150), 1 block
+//   k_update    x_b += gamma D, Ax_b += gamma s23, s11 = sum_k Ax_k - b
+//               (lasso.py:153-155, :105)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bpgl {
+
+constexpr int kThreads = 256;   // 4 waves of 64
+constexpr int kWaves = 4;
+constexpr int kU = 4;           // 16-byte loads per lane per row segment (= kWaves)
+
+struct DevState {
+    long long t;          // index of the next iteration
+    long long done;       // stopping rule fired
+    long long block_cnt;  // lasso.py:144-150
+    long long t_last;     // last t reached (the reference's loop variable)
+    long long cur_mb;     // block updated by the current iteration
+    long long t_base;     // wall clock (100 MHz) at reset
+    double gamma;         // step size of the last iteration
+    double err;           // error criterion of the last iteration
+    double r1, r2;        // line-search numerators (diagnostics)
+    long long iters;      // iterations completed (update applied or stop reached)
+    long long pad[5];
+};
+
+struct Params {
+    const void* A;
+    long long lda, block_stride;
+    long long m, w, wp;
+    int nblock, nseg, nchunk, R;
+    int nparts, nranks, rank, has_comm;
+    double* slab_g;   // [nchunk][wp]
+    double* slab_s;   // [nseg][m]
+    double* g;        // [wp]
+    double* D;        // [wp]
+    double* parts;    // [nparts][4]
+    double* comm;     // [m + 2 + nranks]
+    double* r;        // [m]   residual s11 = sum_k Ax_k - b
+    double* Ax;       // [nblock][m]
+    const double* b;  // [m]
+    double* x;        // [nblock][wp]
+    const double* diag;  // [nblock][wp]
+    const double* rec;   // [nblock][wp]  1 / diag (lasso.py:29-30)
+    const int* order;    // [order_len] or null
+    long long order_len;
+    double* err_iter;
+    double* time_iter;
+    long long rec_len;
+    DevState* st;
+    double mu, err_bound;
+    double wall_tick_s;   // seconds per wall_clock64() tick
+};
+
+// ---------------------------------------------------------------------------
+// 16-byte vector loads of A, widened to fp64
+// ---------------------------------------------------------------------------
+template <typename T> struct VecT;
+template <> struct VecT<float> {
+    static constexpr int N = 4;
+    using raw = float4;
+    __device__ static inline void cvt(const raw& v, double (&o)[N]) {
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    }
+};
+template <> struct VecT<double> {
+    static constexpr int N = 2;
+    using raw = double2;
+    __device__ static inline void cvt(const raw& v, double (&o)[N]) { o[0] = v.x; o[1] = v.y; }
+};
+struct bf16_t { unsigned short u; };
+template <> struct VecT<bf16_t> {
+    static constexpr int N = 8;
+    using raw = uint4;
+    __device__ static inline double one(unsigned int h) { return (double)__uint_as_float(h << 16); }
+    __device__ static inline void cvt(const raw& v, double (&o)[N]) {
+        o[0] = one(v.x & 0xffffu); o[1] = one(v.x >> 16);
+        o[2] = one(v.y & 0xffffu); o[3] = one(v.y >> 16);
+        o[4] = one(v.z & 0xffffu); o[5] = one(v.z >> 16);
+        o[6] = one(v.w & 0xffffu); o[7] = one(v.w >> 16);
+    }
+};
+
+template <typename T>
+__device__ __forceinline__ typename VecT<T>::raw ldv(const T* p) {
+    return *reinterpret_cast<const typename VecT<T>::raw*>(p);
+}
+
+__device__ __forceinline__ int cur_block(const Params& p) {
+    const long long t = p.st->t;
+    if (p.order) return p.order[t < p.order_len ? t : p.order_len - 1];
+    return (int)(t % p.nblock);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { double u = __shfl_xor(v, o); v = (u > v || u != u) ? u : v; }
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// colpass: slab[chunk][col] = sum_{i in chunk} A_b[i][col] * vec[i]   (MODE 0)
+//          slab[chunk][col] = sum_{i in chunk} A_b[i][col]^2           (MODE 1)
+// grid = nseg * nchunk blocks of 256; block (seg, chunk) owns SEGW columns and
+// R rows; the 4 waves split the rows (wave q: rows q, q+4, ...) and sum their
+// fp64 partials through LDS in a fixed order.
+// ---------------------------------------------------------------------------
+template <typename T, int MODE>
+__global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __restrict__ vec,
+                                                      double* __restrict__ slab, int fixed_block) {
+    constexpr int V = VecT<T>::N;
+    constexpr int SEGW = 64 * V * kU;
+    using raw = typename VecT<T>::raw;
+    if (fixed_block < 0 && p.st->done) return;
+    const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
+    const int seg = blockIdx.x % p.nseg;
+    const int chunk = blockIdx.x / p.nseg;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
+
+    long long col[kU];
+    bool ok[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        long long c = (long long)seg * SEGW + u * 64 * V + lane * V;
+        ok[u] = c < p.wp;
+        col[u] = ok[u] ? c : 0;     // clamped: loads stay in bounds, value masked below
+    }
+    double acc[kU][V];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[u][e] = 0.0;
+
+    const long long i0 = (long long)chunk * p.R;
+    const long long i1 = (i0 + p.R < p.m) ? i0 + p.R : p.m;
+    for (long long i = i0 + wave; i < i1; i += 2 * kWaves) {
+        const bool two = i + kWaves < i1;
+        const long long i2 = two ? i + kWaves : i;
+        const T* r0 = Ab + i * p.lda;
+        const T* r1 = Ab + i2 * p.lda;
+        raw a0[kU], a1[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) a0[u] = ldv<T>(r0 + col[u]);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) a1[u] = ldv<T>(r1 + col[u]);
+        double s0 = 1.0, s1 = 1.0;
+        if (MODE == 0) { s0 = vec[i]; s1 = vec[i2]; }   // i2 == i when !two: in bounds
+        s1 = two ? s1 : 0.0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            double v0[V], v1[V];
+            VecT<T>::cvt(a0[u], v0);
+            VecT<T>::cvt(a1[u], v1);
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                if (MODE == 0) {
+                    acc[u][e] = fma(v0[e], s0, acc[u][e]);
+                    acc[u][e] = fma(v1[e], s1, acc[u][e]);
+                } else {
+                    acc[u][e] = fma(v0[e], v0[e], acc[u][e]);
+                    acc[u][e] = fma(v1[e] * s1, v1[e], acc[u][e]);
+                }
+            }
+        }
+    }
+    // cross-wave reduction in a fixed order (wave 0 + 1 + 2 + 3)
+    __shared__ double red[kWaves][kU * V][64];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+        for (int e = 0; e < V; ++e) red[wave][u * V + e][lane] = acc[u][e];
+    __syncthreads();
+    // wave q finalises column group u = q: V consecutive fp64 per lane
+    const int q = wave;
+    const long long c = (long long)seg * SEGW + q * 64 * V + lane * V;
+    if (c < p.wp) {
+        double o[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+            o[e] = ((red[0][q * V + e][lane] + red[1][q * V + e][lane]) + red[2][q * V + e][lane]) +
+                   red[3][q * V + e][lane];
+        double* dst = slab + (long long)chunk * p.wp + c;
+#pragma unroll
+        for (int e = 0; e < V; e += 2) *reinterpret_cast<double2*>(dst + e) = make_double2(o[e], o[e + 1]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// colreduce: out[j] = sum_{c < nchunk} slab[c][j]   (fixed order)   -- diag / mtv API
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_colreduce(const double* __restrict__ slab, long long wp,
+                                                        int nchunk, double* __restrict__ out,
+                                                        double* __restrict__ rec_out) {
+    const long long j = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (j >= wp) return;
+    double s = 0.0;
+    for (int c = 0; c < nchunk; ++c) s += slab[(long long)c * wp + j];
+    out[j] = s;
+    if (rec_out) rec_out[j] = 1.0 / s;
+}
+
+// ---------------------------------------------------------------------------
+// shrink (s14/s15 + error criterion), one thread per column of block mb
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double soft_thr(double t, double tau) {   // cpu_calculation.py:5-6
+    const double mag = fabs(t) - tau;
+    const double sg = t > 0.0 ? 1.0 : (t < 0.0 ? -1.0 : 0.0);
+    return sg * (mag > 0.0 ? mag : 0.0);
+}
+__device__ __forceinline__ double proj(double v, double lo, double hi) {  // cpu_calculation.py:10-11
+    const double a = v < hi ? v : hi;
+    return a > lo ? a : lo;
+}
+
+__global__ __launch_bounds__(kThreads) void k_shrink(Params p) {
+    if (p.st->done) return;
+    const int mb = cur_block(p);
+    const long long j = (long long)blockIdx.x * kThreads + threadIdx.x;
+    double abx = 0.0, ax = 0.0, err = 0.0;
+    if (j < p.wp) {
+        double g = 0.0;
+        for (int c = 0; c < p.nchunk; ++c) g += p.slab_g[(long long)c * p.wp + j];
+        p.g[j] = g;
+        double Dj = 0.0;
+        if (j < p.w) {
+            const long long k = (long long)mb * p.wp + j;
+            const double d = p.diag[k], xj = p.x[k];
+            const double rx = d * xj - g;                     // lasso.py:114
+            const double bx = p.rec[k] * soft_thr(rx, p.mu);  // lasso.py:115-117
+            Dj = bx - xj;                                     // lasso.py:119
+            abx = fabs(bx);
+            ax = fabs(xj);
+            err = fabs(g - proj(g - xj, -p.mu, p.mu));        // cpu_calculation.py:15-20
+        }
+        p.D[j] = Dj;
+    }
+    // block reduction (fixed order): wave shuffles then 4 wave results
+    __shared__ double sred[3][kWaves];
+    abx = wave_sum(abx);
+    ax = wave_sum(ax);
+    err = wave_max(err);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { sred[0][wave] = abx; sred[1][wave] = ax; sred[2][wave] = err; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
+        double b = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
+        double e = sred[2][0];
+        for (int q = 1; q < kWaves; ++q) e = (sred[2][q] > e || sred[2][q] != sred[2][q]) ? sred[2][q] : e;
+        double* dst = p.parts + 4ll * blockIdx.x;
+        dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// rowpass: slab_s[seg][i] = sum_{j in seg} A_b[i][j] * d[j]
+// Each wave owns rows wave, wave+4, ... of the chunk, four rows per trip; the
+// four per-lane partials are reduced with a transposed butterfly (7 fp64
+// shuffles per 4 rows instead of 24): lanes 0/16/32/48 end with rows 0..3.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __restrict__ d,
+                                                      double* __restrict__ slab, int fixed_block) {
+    constexpr int V = VecT<T>::N;
+    constexpr int SEGW = 64 * V * kU;
+    using raw = typename VecT<T>::raw;
+    if (fixed_block < 0 && p.st->done) return;
+    const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
+    const int seg = blockIdx.x % p.nseg;
+    const int chunk = blockIdx.x / p.nseg;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
+
+    long long col[kU];
+    double dv[kU][V];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const long long c = (long long)seg * SEGW + u * 64 * V + lane * V;
+        const bool ok = c < p.wp;
+        col[u] = ok ? c : 0;
+#pragma unroll
+        for (int e = 0; e < V; ++e) dv[u][e] = d[col[u] + e];
+#pragma unroll
+        for (int e = 0; e < V; ++e) dv[u][e] = ok ? dv[u][e] : 0.0;
+    }
+    const long long i0 = (long long)chunk * p.R;
+    const long long i1 = (i0 + p.R < p.m) ? i0 + p.R : p.m;
+    double* out = slab + (long long)seg * p.m;
+    for (long long ib = i0 + wave; ib < i1; ib += 4 * kWaves) {
+        long long rows[4];
+        const T* rp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            rows[k] = ib + k * kWaves;
+            rp[k] = Ab + (rows[k] < i1 ? rows[k] : ib) * p.lda;
+        }
+        raw a[4][kU];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int u = 0; u < kU; ++u) a[k][u] = ldv<T>(rp[k] + col[u]);
+        double ps[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double s = 0.0;
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                double v[V];
+                VecT<T>::cvt(a[k][u], v);
+#pragma unroll
+                for (int e = 0; e < V; ++e) s = fma(v[e], dv[u][e], s);
+            }
+            ps[k] = s;
+        }
+        // transposed butterfly over the 64 lanes
+        const bool up = lane & 32;
+        const double k0 = up ? ps[2] : ps[0], k1 = up ? ps[3] : ps[1];
+        const double s0 = up ? ps[0] : ps[2], s1 = up ? ps[1] : ps[3];
+        const double q0 = k0 + __shfl_xor(s0, 32);
+        const double q1 = k1 + __shfl_xor(s1, 32);
+        const bool hb = lane & 16;
+        double v = (hb ? q1 : q0) + __shfl_xor(hb ? q0 : q1, 16);
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 1);
+        if ((lane & 15) == 0) {
+            const int k = (up ? 2 : 0) + (hb ? 1 : 0);
+            const long long row = ib + k * kWaves;
+            if (row < i1) out[row] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// rowreduce: out[i] = sum_{q < nseg} slab_s[q][i]; with `solver` set, block 0
+// also folds the shrink partials into out[m], out[m+1], out[m+2+rank].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* __restrict__ slab,
+                                                        double* __restrict__ out, int solver) {
+    if (solver && p.st->done) return;
+    const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (i < p.m) {
+        double s = 0.0;
+        for (int q = 0; q < p.nseg; ++q) s += slab[(long long)q * p.m + i];
+        out[i] = s;
+    }
+    if (solver && blockIdx.x == 0) {
+        __shared__ double sred[3][kWaves];
+        double a = 0.0, b = 0.0, e = 0.0;
+        for (int k = threadIdx.x; k < p.nparts; k += kThreads) {
+            a += p.parts[4ll * k];
+            b += p.parts[4ll * k + 1];
+            const double ek = p.parts[4ll * k + 2];
+            e = (ek > e || ek != ek) ? ek : e;
+        }
+        a = wave_sum(a);
+        b = wave_sum(b);
+        e = wave_max(e);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) { sred[0][wave] = a; sred[1][wave] = b; sred[2][wave] = e; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            a = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
+            b = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
+            e = sred[2][0];
+            for (int q = 1; q < kWaves; ++q) e = (sred[2][q] > e || sred[2][q] != sred[2][q]) ? sred[2][q] : e;
+            out[p.m] = a;
+            out[p.m + 1] = b;
+            for (int r = 0; r < p.nranks; ++r) out[p.m + 2 + r] = (r == p.rank) ? e : 0.0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// step: exact line search (lasso.py:129-136) + stopping rule (lasso.py:141-150)
+// one block of 1024 threads; fixed-order reductions.
+// ---------------------------------------------------------------------------
+constexpr int kStepThreads = 1024;
+__global__ __launch_bounds__(kStepThreads) void k_step(Params p) {
+    if (p.st->done) return;
+    const double* s23 = p.comm;
+    double a = 0.0, b = 0.0;
+    for (long long i = threadIdx.x; i < p.m; i += kStepThreads) {
+        const double s = s23[i];
+        a = fma(p.r[i], s, a);
+        b = fma(s, s, b);
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    __shared__ double sa[kStepThreads / 64], sb[kStepThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { sa[wave] = a; sb[wave] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r1 = 0.0, r2 = 0.0;
+        for (int q = 0; q < kStepThreads / 64; ++q) { r1 += sa[q]; r2 += sb[q]; }
+        r1 += p.mu * (s23[p.m] - s23[p.m + 1]);             // mu (||Bx||_1 - ||x_m||_1)
+        double err = s23[p.m + 2];
+        for (int r = 1; r < p.nranks; ++r) {
+            const double e = s23[p.m + 2 + r];
+            err = (e > err || e != e) ? e : err;
+        }
+        double gamma = (r2 == 0.0) ? 0.0 : proj(-r1 / r2, 0.0, 1.0);
+        DevState* st = p.st;
+        const long long t = st->t;
+        const int mb = cur_block(p);
+        if (p.err_iter && t < p.rec_len) p.err_iter[t] = err;
+        st->r1 = r1;
+        st->r2 = r2;
+        st->err = err;
+        st->t_last = t;
+        st->cur_mb = mb;
+        if (p.err_bound >= 0.0) {
+            if (err < p.err_bound) st->block_cnt += 1;
+            if (mb == p.nblock - 1) {
+                if (st->block_cnt == p.nblock) {
+                    st->done = 1;
+                    st->gamma = 0.0;
+                    st->iters = t + 1;
+                    return;
+                }
+                st->block_cnt = 0;
+            }
+        }
+        st->gamma = gamma;
+        st->t = t + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// update: x_b += gamma D (lasso.py:153), Ax_b += gamma s23 (lasso.py:155),
+// next residual s11 = sum_k Ax_k - b (lasso.py:105)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_update(Params p) {
+    if (p.st->done) return;
+    const double gamma = p.st->gamma;
+    const int mb = (int)p.st->cur_mb;
+    const long long n = p.wp > p.m ? p.wp : p.m;
+    for (long long k = (long long)blockIdx.x * kThreads + threadIdx.x; k < n;
+         k += (long long)gridDim.x * kThreads) {
+        if (k < p.w) p.x[(long long)mb * p.wp + k] += gamma * p.D[k];
+        if (k < p.m) {
+            p.Ax[(long long)mb * p.m + k] += gamma * p.comm[k];
+            double acc = p.Ax[k];
+            for (int q = 1; q < p.nblock; ++q) acc += p.Ax[(long long)q * p.m + k];
+            p.r[k] = acc - p.b[k];
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const long long t = p.st->t - 1;
+        p.st->iters = t + 1;
+        if (p.time_iter && t < p.rec_len)
+            p.time_iter[t + 1] = (double)(wall_clock64() - p.st->t_base) * p.wall_tick_s;
+    }
+}
+
+// residual from scratch: r = sum_k Ax_k - b; state init
+__global__ __launch_bounds__(kThreads) void k_reset(Params p) {
+    for (long long k = (long long)blockIdx.x * kThreads + threadIdx.x; k < p.m;
+         k += (long long)gridDim.x * kThreads) {
+        double acc = p.Ax[k];
+        for (int q = 1; q < p.nblock; ++q) acc += p.Ax[(long long)q * p.m + k];
+        p.r[k] = acc - p.b[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        DevState* st = p.st;
+        st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0;
+        st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0;
+        st->t_base = (long long)wall_clock64();
+        if (p.time_iter) p.time_iter[0] = 0.0;
+    }
+}
+
+}  // namespace bpgl

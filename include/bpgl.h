@@ -1,0 +1,161 @@
+/*
+ * bpgl -- MI355X-native block proximal-gradient (best-response) lasso hot path.
+ *
+ * Flat C ABI of convex_optimization_amd/_lib/libbpgl.so.  Plain pointers and
+ * sizes only; every device pointer is memory allocated by the caller (PyTorch
+ * tensors on the Python side).  The library never calls hipMalloc: it borrows
+ * the caller's buffers for the lifetime of a context.
+ *
+ * Problem (reference lasso.py:102-157, one "ISTA iteration" = one block update):
+ *   minimise 1/2 ||A x - b||^2 + mu ||x||_1,  A: m x n, columns split into
+ *   nblock feature blocks of width w = n / nblock.
+ *
+ * Device layout of A (one rank): element (i, j) of feature block b lives at
+ *   A + b * block_stride + i * lda + j        (0 <= j < w_pad)
+ * w_pad = w rounded up to 16 bytes worth of elements; padding columns must be 0.
+ * The reference's own GPU layout (gpu_calculation.py:172-173, np.hsplit into a
+ * (BLOCK, H, W) array) is block_stride = m * w_pad, lda = w_pad.
+ *
+ * Conventions: return 0 on success, a negative BPGL_E* code on failure; the
+ * failing call's message is available from bpgl_last_error() (thread-local).
+ * No C++ exception crosses this boundary.  A context is not thread-safe and is
+ * bound to one device; all work is enqueued on the context's stream.
+ */
+#ifndef BPGL_H
+#define BPGL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* dtype of A (the reference's class tunable TYPE, gpu_calculation.py:146) */
+enum { BPGL_F32 = 0, BPGL_F64 = 1, BPGL_BF16 = 2 };
+
+enum {
+    BPGL_OK = 0,
+    BPGL_E_ARG = -1,      /* bad argument / shape / alignment            */
+    BPGL_E_STATE = -2,    /* call out of order (not bound / no solver)   */
+    BPGL_E_HIP = -3,      /* HIP runtime error                           */
+    BPGL_E_RCCL = -4,     /* RCCL error                                  */
+    BPGL_E_SCRATCH = -5   /* scratch buffer too small                    */
+};
+
+typedef struct bpgl_ctx bpgl_ctx;
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* bpgl_last_error(void);
+
+/* Library / ABI version (major * 10000 + minor * 100 + patch). */
+int bpgl_version(void);
+
+/*
+ * Create a context for an m x n_local matrix split into nblock feature blocks.
+ * Replaces GPU_Calculation.__init__ / init_cpu_array (gpu_calculation.py:148-220):
+ * grid sizes and scratch needs are derived here instead of per-call numpy.
+ * `hip_stream` may be NULL (the library then creates its own stream).
+ */
+int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_local,
+                int32_t nblock, void* hip_stream);
+void bpgl_destroy(bpgl_ctx* ctx);
+
+/* The stream all work of this context is enqueued on. */
+void* bpgl_stream(bpgl_ctx* ctx);
+
+/* Bytes of device scratch the caller must provide to bpgl_bind. */
+int64_t bpgl_scratch_bytes(const bpgl_ctx* ctx);
+
+/* Padded block width (w rounded up to a 16-byte multiple of elements). */
+int64_t bpgl_block_width_padded(const bpgl_ctx* ctx);
+
+/*
+ * Bind the device copy of A and a scratch buffer (both caller-owned).
+ * Replaces init_gpu_array (gpu_calculation.py:222-236), whose H2D copy and
+ * pycuda allocations become caller-side PyTorch allocations.
+ */
+int bpgl_bind(bpgl_ctx* ctx, const void* A, int64_t lda, int64_t block_stride,
+              void* scratch, int64_t scratch_bytes);
+
+/*
+ * diag(A_b^T A_b) for every block b into out[b * w_pad + j] (device, fp64).
+ * Replaces GPU_Calculation.diag_ATA + kernel get_diag_ATA
+ * (gpu_calculation.py:246-261, :116-137).  Also caches 1/diag for the solver.
+ */
+int bpgl_diag_ata(bpgl_ctx* ctx, double* out);
+
+/*
+ * g = A_b^T r  (device: r has m fp64 values, g receives w_pad fp64 values).
+ * Replaces GPU_Calculation.mat_tMulVec_DiffSize + kernel mul_mat_t_vec_diffsize
+ * (gpu_calculation.py:264-277, :20-55); the split-K reduction happens on the
+ * device in a fixed order (no host partial sums, no atomics).
+ */
+int bpgl_mtv(bpgl_ctx* ctx, int32_t block, const double* r, double* g);
+
+/*
+ * s = A_b d  (device: d has w_pad fp64 values, s receives m fp64 values).
+ * Replaces GPU_Calculation.matMulVec_DiffSize + kernel mul_mat_vec_diffsize
+ * (gpu_calculation.py:280-292, :58-91).
+ */
+int bpgl_mv(bpgl_ctx* ctx, int32_t block, const double* d, double* s);
+
+/*
+ * Multi-GPU: column shards of every feature block across ranks (the
+ * reference's P-way shards, cpu_calculation.py:23-27 / lasso.py:107-126,
+ * lifted from Pool workers to GPUs).  bpgl_comm_unique_id fills 128 bytes on
+ * one rank; the caller broadcasts them; every rank then calls bpgl_comm_init.
+ * The solver then all-reduces (RCCL, SUM) m + 2 + nranks fp64 values per
+ * iteration.
+ */
+int bpgl_comm_unique_id(void* out128);
+int bpgl_comm_init(bpgl_ctx* ctx, const void* unique_id128, int rank, int nranks);
+
+/*
+ * Device-resident solver (the loop of ClassLasso.run, lasso.py:190-292, and
+ * ClassLassoCB_v2.run, lasso.py:458-613, with every step on the device).
+ *
+ * bpgl_solver_reset: b (m, device fp64), x (nblock * w_pad, device fp64, in/out,
+ *   initial point), order (device int32 block index per iteration, NULL =
+ *   cyclic t % nblock as lasso.py:40-41), order_len, err_bound (< 0 disables
+ *   the ERR_BOUND stopping rule of lasso.py:141-150), err_iter / time_iter
+ *   (device fp64, NULL = not recorded; record_len entries of err_iter and
+ *   record_len + 1 of time_iter, as lasso.py:54-62).
+ * bpgl_solver_step: enqueue n_iter more iterations (asynchronous; replays a
+ *   captured hipGraph of one iteration when `use_graph` was set).
+ * bpgl_solver_status: synchronise the stream and read (iterations done,
+ *   stopped flag, last t, last step size, last error).
+ * bpgl_solver_residual: device pointer of the residual s11 = sum_k Ax_k - b (m).
+ */
+int bpgl_solver_reset(bpgl_ctx* ctx, const double* b, double mu, double* x,
+                      const int32_t* order, int64_t order_len, double err_bound,
+                      double* err_iter, double* time_iter, int64_t record_len,
+                      int use_graph);
+int bpgl_solver_step(bpgl_ctx* ctx, int64_t n_iter);
+int bpgl_solver_status(bpgl_ctx* ctx, int64_t* iters_done, int* stopped, int64_t* t_last,
+                       double* gamma, double* err);
+const double* bpgl_solver_residual(bpgl_ctx* ctx);
+
+/*
+ * One-call form: reset, run n_iter iterations, wait, report.  The survey's
+ * bpgl_iterate.  iters_done may be NULL.
+ */
+int bpgl_iterate(bpgl_ctx* ctx, int64_t n_iter, const int32_t* order, double mu,
+                 const double* b, double* x, double* err_iter, double* time_iter,
+                 double err_bound, int64_t* iters_done);
+
+/* Timing of the most recent bpgl_solver_step window on the context stream:
+ * average duration (ms) of each kernel kind over the window, measured with
+ * HIP events when profiling was enabled by bpgl_set_kernel_timing(ctx, 1).
+ * kinds: 0 colpass (A^T r), 1 shrink, 2 rowpass (A D), 3 rowreduce, 4 step,
+ * 5 update, 6 allreduce. */
+int bpgl_set_kernel_timing(bpgl_ctx* ctx, int enable);
+int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 7 */, int64_t* samples);
+
+/* Launch geometry chosen for this context (diagnostics). */
+int bpgl_geometry(const bpgl_ctx* ctx, int32_t* nseg, int32_t* nchunk, int32_t* rows_per_chunk,
+                  int32_t* seg_width);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPGL_H */

@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+This script is the only place that touches /root/reference, and it runs only in
+the build container (the GPU box has no /root/reference). It imports the
+reference's own modules:
+
+  * cpu_calculation.py  -- imported as-is (numpy only) for per-function KATs;
+  * parameters.py       -- the problem generator, with ``parameters.time`` pinned
+                           to a constant so ``np.random.seed(int(time()))``
+                           (parameters.py:17) becomes a fixed seed;
+  * lasso.py            -- ``ClassLassoCPU`` (lasso.py:25-169) runs unmodified.
+                           lasso.py imports pycuda/skcuda at module scope
+                           (lasso.py:13-16) although ClassLassoCPU never uses
+                           them; those absent packages are given empty module
+                           objects so the import succeeds.
+
+``ClassLassoCPU.run`` does not return x (lasso.py:167-169), so the final
+``x``/``t`` locals of ``run`` are captured with ``sys.setprofile``.
+
+A is NOT stored: it is regenerated bit-exactly by
+``RandomState(seed).randn(N, K)`` row-normalised (the first draw after
+``np.random.seed(seed)`` in parameters.py:17-21); every fixture stores a
+checksum of A so a regeneration mismatch is detected.
+
+Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
+"""
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference():
+    for name in ("pycuda", "pycuda.driver", "pycuda.autoinit", "pycuda.compiler",
+                 "pycuda.gpuarray", "pycuda.elementwise", "skcuda", "skcuda.cublas"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["pycuda"].gpuarray = sys.modules["pycuda.gpuarray"]
+    sys.modules["pycuda.elementwise"].ElementwiseKernel = None
+    sys.modules["skcuda"].cublas = sys.modules["skcuda.cublas"]
+    sys.path.insert(0, REF)
+    import cpu_calculation  # noqa: E402
+    import parameters  # noqa: E402
+    import lasso  # noqa: E402
+    return cpu_calculation, parameters, lasso
+
+
+def a_checksum(A):
+    return np.array([A.sum(), np.square(A).sum(), A[0, 0], A[-1, -1],
+                     A[A.shape[0] // 2, A.shape[1] // 3]], dtype=np.float64)
+
+
+def regen_A(seed, N, K):
+    """Mirror of parameters.py:17-20 (first RNG draw after the seed)."""
+    A = np.random.RandomState(seed).randn(N, K)
+    return A / (np.linalg.norm(A, ord=2, axis=1, keepdims=True))
+
+
+def run_reference(lasso, cpu_calculation, A, b, mu, BLOCK, P, ITER_MAX,
+                  err_bound=None, order_cls=None, py_seed=None):
+    """Run reference ClassLassoCPU (or a random-order subclass) and capture x."""
+    A_block_p = cpu_calculation.A_bp_get(A, BLOCK, P)
+    d_ATA = cpu_calculation.fun_diag_ATA(A_block_p)
+    cls = order_cls or lasso.ClassLassoCPU
+    obj = cls(A_block_p, d_ATA, A, b, mu, BLOCK, P, ITER_MAX)
+    err_iter = np.zeros(ITER_MAX)
+    time_iter = np.zeros(ITER_MAX + 1)
+    captured = {}
+    order = []
+    run_code = lasso.ClassLassoCPU.run.__code__
+    idx_code = cls.index_get.__code__
+
+    def prof(frame, event, arg):
+        if event == "return" and frame.f_code is run_code:
+            captured["x"] = np.array(frame.f_locals["x"])
+            captured["t"] = int(frame.f_locals["t"])
+        if event == "return" and frame.f_code is idx_code:
+            order.append(int(arg))
+
+    if py_seed is not None:
+        random.seed(py_seed)
+    sys.setprofile(prof)
+    try:
+        obj.run(ERR_BOUND=err_bound, err_iter=err_iter, time_iter=time_iter,
+                SILENCE=True, DEBUG=False)
+    finally:
+        sys.setprofile(None)
+    return dict(x=captured["x"], t_last=captured["t"], err_iter=err_iter,
+                order=np.array(order, dtype=np.int32), d_ATA=d_ATA)
+
+
+def make_case(mods, name, seed, N, K, den, BLOCK, P, ITER_MAX, f32_inputs,
+              err_bound=None, random_order=False, py_seed=None):
+    cpu_calculation, parameters, lasso = mods
+    parameters.time = lambda: seed          # pins np.random.seed(int(time()))
+    A, x_true, b, mu = parameters.parameters(N, K, den, False, False, SILENCE=True)
+    A_re = regen_A(seed, N, K)
+    assert np.array_equal(A, A_re), "A regeneration mismatch"
+    if f32_inputs:
+        # fp32-rounded instance: the GPU stores A (and b) in fp32; the reference
+        # then runs in fp64 on exactly those values.
+        A = A.astype(np.float32).astype(np.float64)
+        b = b.astype(np.float32).astype(np.float64)
+        mu = 0.1 * np.max(np.abs(A.T @ b))     # parameters.py:33 on the rounded data
+    order_cls = None
+    if random_order:
+        class ClassLassoCPUR(lasso.ClassLassoCPU):   # lasso.py:296-306 order on the CPU loop
+            index_get = lasso.ClassLassoR.index_get
+
+            def __init__(self, *a):
+                lasso.ClassLassoCPU.__init__(self, *a)
+                self.idx_shuffle = np.arange(self.BLOCK)
+        order_cls = ClassLassoCPUR
+    res = run_reference(lasso, cpu_calculation, A, b, mu, BLOCK, P, ITER_MAX,
+                        err_bound=err_bound, order_cls=order_cls, py_seed=py_seed)
+    iters = res["t_last"] + 1
+    stopped = err_bound is not None and res["t_last"] < ITER_MAX - 1
+    out = dict(seed=np.int64(seed), N=np.int64(N), K=np.int64(K), den=np.float64(den),
+               BLOCK=np.int64(BLOCK), P=np.int64(P), ITER_MAX=np.int64(ITER_MAX),
+               f32_inputs=np.bool_(f32_inputs), b=b, mu=np.float64(mu),
+               x=res["x"], err_iter=res["err_iter"], t_last=np.int64(res["t_last"]),
+               order=res["order"], d_ATA=res["d_ATA"], A_checksum=a_checksum(A),
+               err_bound=np.float64(-1.0 if err_bound is None else err_bound),
+               random_order=np.bool_(random_order), stopped=np.bool_(stopped))
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print(f"{name}: N={N} K={K} BLOCK={BLOCK} P={P} iters={iters} "
+          f"mu={mu:.6f} |x|={np.linalg.norm(res['x']):.6f} err_last={res['err_iter'][res['t_last']]:.3e}")
+
+
+def make_kats(mods):
+    """Per-function known-answer vectors for cpu_calculation.py:5-50."""
+    cpu_calculation = mods[0]
+    rs = np.random.RandomState(7)
+    t = rs.randn(64, 1) * 2
+    v = rs.randn(64, 1)
+    x = rs.randn(64, 1)
+    A = rs.randn(24, 48)
+    s11 = rs.randn(24, 1)
+    BLOCK, P = 2, 3
+    A_bp = cpu_calculation.A_bp_get(A, BLOCK, P)
+    d = rs.randn(48 // BLOCK, 1)
+    out = dict(
+        t=t, tau=np.float64(0.7), soft=cpu_calculation.soft_thresholding(t, 0.7),
+        v=v, proj=cpu_calculation.element_proj(v, -0.3, 0.5),
+        g=t, x=x, mu=np.float64(0.4), err=np.float64(cpu_calculation.error_crit(t, x, 0.4)),
+        A=A, BLOCK=np.int64(BLOCK), P=np.int64(P), A_bp=np.ascontiguousarray(A_bp),
+        s11=s11, s12=np.stack([cpu_calculation.fun_s12(A_bp[0, p], s11) for p in range(P)]),
+        diag=cpu_calculation.fun_diag_ATA(A_bp),
+        d=d, dd_p=cpu_calculation.fun_dd_p(P, d),
+        s22=np.stack([cpu_calculation.fun_s22(A_bp[1, p], cpu_calculation.fun_dd_p(P, d)[p])
+                      for p in range(P)]),
+    )
+    np.savez_compressed(os.path.join(OUT, "kats.npz"), **out)
+    print("kats: written")
+
+
+def main():
+    mods = _import_reference()
+    make_kats(mods)
+    # config 1 (BASELINE.json configs[0]): m=512 n=2048 fp64, 200 iterations
+    make_case(mods, "c1_b1_p1_f64", 20190325, 512, 2048, 0.4, 1, 1, 200, False)
+    make_case(mods, "c1_b2_p4_f64", 20190325, 512, 2048, 0.4, 2, 4, 200, False)
+    # fp32-rounded inputs (GPU fp32 storage parity)
+    make_case(mods, "c1_b1_p1_f32in", 20190326, 512, 2048, 0.4, 1, 1, 200, True)
+    make_case(mods, "c1_b2_p4_f32in", 20190326, 512, 2048, 0.4, 2, 4, 200, True)
+    # ragged / odd shapes: rows not a multiple of anything, narrow blocks
+    make_case(mods, "ragged_b3_p2_f32in", 4242, 77, 120, 0.4, 3, 2, 60, True)
+    # ERR_BOUND stopping (lasso.py:141-150)
+    make_case(mods, "bound_b4_p2_f32in", 99, 96, 320, 0.3, 4, 2, 2000, True,
+              err_bound=1e-3)
+    # random block order (lasso.py:303-306), seeded stdlib random
+    make_case(mods, "random_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 64, True,
+              random_order=True, py_seed=5)
+
+
+if __name__ == "__main__":
+    main()

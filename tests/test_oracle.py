@@ -1,0 +1,89 @@
+"""The oracle (C + numpy restatements) pinned against the reference's own outputs.
+
+Fixtures: tests/golden/*.npz, written by tests/golden/make_golden.py, which ran
+the reference's ClassLassoCPU (lasso.py:25-169) and cpu_calculation.py in the
+build container.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_cases
+from oracle import oracle
+
+# The reference sums with OpenBLAS dgemv / numpy pairwise order; the restatement
+# sums in a fixed row order.  Both are fp64: the measured gap is <= 1e-10.
+X_TOL = 1e-9
+
+
+def _run_args(fx):
+    order = fx["order"] if bool(fx["random_order"]) else None
+    eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
+    return order, eb
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_c_oracle_matches_reference(golden, case):
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    order, eb = _run_args(fx)
+    res = oracle.run(A, fx["b"], fx["mu"], int(fx["BLOCK"]), int(fx["ITER_MAX"]), P=int(fx["P"]),
+                     order=order, err_bound=eb)
+    x = fx["x"].reshape(-1)
+    assert res["t_last"] == int(fx["t_last"])
+    assert np.linalg.norm(res["x"] - x) <= X_TOL * np.linalg.norm(x)
+    T = int(fx["t_last"]) + 1
+    np.testing.assert_allclose(res["err_iter"][:T], fx["err_iter"][:T], rtol=1e-4, atol=1e-10)
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_numpy_oracle_matches_reference(golden, case):
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    order, eb = _run_args(fx)
+    res = oracle.run_numpy(A, fx["b"], fx["mu"], int(fx["BLOCK"]), int(fx["ITER_MAX"]),
+                           order=order, err_bound=eb)
+    x = fx["x"].reshape(-1)
+    assert res["t_last"] == int(fx["t_last"])
+    assert np.linalg.norm(res["x"] - x) <= X_TOL * np.linalg.norm(x)
+
+
+@pytest.mark.parametrize("case", ["c1_b1_p1_f32in", "ragged_b3_p2_f32in"])
+def test_c_oracle_fp32_storage_is_exact(golden, case):
+    """fp32-rounded fixtures: storing A as float32 changes nothing (same values)."""
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    r64 = oracle.run(A, fx["b"], fx["mu"], int(fx["BLOCK"]), 40, P=int(fx["P"]))
+    r32 = oracle.run(A.astype(np.float32), fx["b"], fx["mu"], int(fx["BLOCK"]), 40, P=int(fx["P"]))
+    np.testing.assert_array_equal(r64["x"], r32["x"])
+
+
+def test_c_oracle_thread_count_invariant(golden):
+    fx = golden("c1_b2_p4_f64")
+    A = oracle.fixture_A(fx)
+    a = oracle.run(A, fx["b"], fx["mu"], 2, 30, P=4, nthreads=1)
+    b = oracle.run(A, fx["b"], fx["mu"], 2, 30, P=4, nthreads=5)
+    np.testing.assert_array_equal(a["x"], b["x"])
+
+
+def test_oracle_kernels_match_reference_kats(golden):
+    k = golden("kats")
+    A, BLOCK, P = k["A"], int(k["BLOCK"]), int(k["P"])
+    K = A.shape[1]
+    w, ws = K // BLOCK, K // (BLOCK * P)
+    # fun_diag_ATA
+    np.testing.assert_allclose(oracle.diag_ata(A, BLOCK), k["diag"], rtol=1e-13)
+    # fun_s12 per shard of block 0
+    for p in range(P):
+        np.testing.assert_allclose(oracle.mtv(A, p * ws, ws, k["s11"]), k["s12"][p].reshape(-1), rtol=1e-12)
+    # sum over shards of fun_s22 of block 1 == oracle mv with P shards
+    s = oracle.mv(A, w, w, k["d"], P=P)
+    np.testing.assert_allclose(s, k["s22"].sum(axis=0).reshape(-1), rtol=1e-12, atol=1e-14)
+
+
+def test_sharded_decomposition_equals_single(golden):
+    """The P-shard (future multi-GPU) decomposition is numerically the single-shard algorithm."""
+    fx = golden("c1_b1_p1_f32in")
+    A = oracle.fixture_A(fx)
+    a = oracle.run(A, fx["b"], fx["mu"], 1, 100, P=1)
+    b = oracle.run(A, fx["b"], fx["mu"], 1, 100, P=8)
+    assert np.linalg.norm(a["x"] - b["x"]) <= 1e-10 * np.linalg.norm(a["x"])
