@@ -55,6 +55,7 @@ _SIGS = {
     "bpgl_solver_residual": (_p, [_p]),
     "bpgl_iterate": (_int, [_p, _i64, _p, _f64, _p, _p, _p, _p, _f64, ctypes.POINTER(_i64)]),
     "bpgl_set_kernel_timing": (_int, [_p, _int]),
+    "bpgl_set_tuning": (_int, [_p, ctypes.c_char_p, _i64]),
     "bpgl_kernel_times": (_int, [_p, ctypes.POINTER(_f64), ctypes.POINTER(_i64)]),
     "bpgl_geometry": (_int, [_p, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                              ctypes.POINTER(_i32)]),

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -79,6 +80,7 @@ struct bpgl_ctx {
     std::vector<hipEvent_t> evs;   // (kinds + 1) events per timed iteration
     int64_t timed_iters = 0;
     double wall_tick_s = 1e-8;
+    int reverse_rows = 1;
 };
 
 namespace {
@@ -89,13 +91,14 @@ void geometry(bpgl_ctx* c) {
     c->wp = up(c->w, V);
     c->nseg = (int)cdiv(c->wp, c->segw);
     // ~8 blocks per CU on 256 CUs, rows per chunk a multiple of 16 (4 waves x 4 rows)
-    const int64_t target = 2048;
+    int64_t target = 2048;
+    if (const char* e = getenv("BPGL_TARGET_BLOCKS")) target = std::max<int64_t>(1, atoll(e));
     int64_t nchunk = std::max<int64_t>(1, cdiv(target, c->nseg));
     nchunk = std::min<int64_t>(nchunk, cdiv(c->m, 16));
     int64_t R = up(cdiv(c->m, nchunk), 16);
     c->R = (int)R;
     c->nchunk = (int)cdiv(c->m, R);
-    c->nparts = (int)cdiv(c->wp, kThreads);
+    c->nparts = (int)cdiv(c->wp, kColsPerShrink);
 }
 
 struct Carve {
@@ -109,7 +112,7 @@ struct Carve {
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, comm, r, Ax, st, diag, rec, total;
+    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -120,6 +123,7 @@ Layout layout(const bpgl_ctx* c) {
     L.g = k.take(8 * c->wp);
     L.D = k.take(8 * c->wp);
     L.parts = k.take(8 * 4 * (int64_t)c->nparts);
+    L.parts2 = k.take(8 * 2 * cdiv(c->m, kRowsPerReduce));
     L.comm = k.take(8 * (c->m + 2 + kMaxRanks));
     L.r = k.take(8 * c->m);
     L.Ax = k.take(8 * (int64_t)c->nblock * c->m);
@@ -161,9 +165,9 @@ int rowpass(bpgl_ctx* c, const double* d, double* slab, int fixed_block) {
     }
 }
 
-int rowreduce(bpgl_ctx* c, const double* slab, double* out, int solver) {
-    hipLaunchKernelGGL(k_rowreduce, dim3((unsigned)cdiv(c->m, kThreads)), dim3(kThreads), 0, c->stream,
-                       c->p, slab, out, solver);
+int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) {
+    hipLaunchKernelGGL(k_rowreduce, dim3((unsigned)cdiv(c->m, kRowsPerReduce)), dim3(kThreads), 0, c->stream,
+                       c->p, slab, out, mode);
     LAUNCH_CHECK("k_rowreduce");
     return 0;
 }
@@ -174,9 +178,11 @@ int check_ready(const bpgl_ctx* c) {
     return 0;
 }
 
-void ev_record(bpgl_ctx* c, int64_t it, int k) {
+// kinds: 0 colpass, 1 shrink, 2 rowpass, 3 rowreduce, 4 allreduce, 5 step, 6 update;
+// event 2 * (it * kinds + kind) + {0: start, 1: end}
+void ev_record(bpgl_ctx* c, int64_t it, int kind, int end) {
     if (!c->timing) return;
-    const size_t idx = (size_t)it * (kTimedKinds + 1) + k;
+    const size_t idx = 2 * ((size_t)it * kTimedKinds + kind) + end;
     while (c->evs.size() <= idx) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return;
@@ -188,32 +194,39 @@ void ev_record(bpgl_ctx* c, int64_t it, int k) {
 // One block update, enqueued on c->stream.  The block index and every
 // iteration-dependent value are read on the device from the state words, so
 // the same launch sequence (or its captured graph) serves every iteration.
-int enqueue_iteration(bpgl_ctx* c, int64_t timed_it) {
+int enqueue_iteration(bpgl_ctx* c, int64_t it) {
     int rc;
-    ev_record(c, timed_it, 0);
+    const bool multi = c->comm != nullptr;
+    ev_record(c, it, 0, 0);
     if ((rc = colpass(c, 0, c->p.r, c->p.slab_g, -1))) return rc;
-    ev_record(c, timed_it, 1);
+    ev_record(c, it, 0, 1);
+    ev_record(c, it, 1, 0);
     hipLaunchKernelGGL(k_shrink, dim3((unsigned)c->nparts), dim3(kThreads), 0, c->stream, c->p);
     LAUNCH_CHECK("k_shrink");
-    ev_record(c, timed_it, 2);
+    ev_record(c, it, 1, 1);
+    ev_record(c, it, 2, 0);
     if ((rc = rowpass(c, c->p.D, c->p.slab_s, -1))) return rc;
-    ev_record(c, timed_it, 3);
-    if ((rc = rowreduce(c, c->p.slab_s, c->p.comm, 1))) return rc;
-    ev_record(c, timed_it, 4);
-    if (c->comm) {
+    ev_record(c, it, 2, 1);
+    ev_record(c, it, 3, 0);
+    if ((rc = rowreduce(c, c->p.slab_s, c->p.comm, multi ? 2 : 1))) return rc;
+    ev_record(c, it, 3, 1);
+    if (multi) {
+        ev_record(c, it, 4, 0);
         ncclResult_t nr = ncclAllReduce(c->p.comm, c->p.comm, (size_t)(c->m + 2 + c->nranks), ncclFloat64,
                                         ncclSum, c->comm, c->stream);
         if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
+        ev_record(c, it, 4, 1);
+        ev_record(c, it, 5, 0);
+        hipLaunchKernelGGL(k_step, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_step");
+        ev_record(c, it, 5, 1);
     }
-    ev_record(c, timed_it, 5);
-    hipLaunchKernelGGL(k_step, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_step");
-    ev_record(c, timed_it, 6);
+    ev_record(c, it, 6, 0);
     const int64_t nupd = std::max<int64_t>(c->wp, c->m);
     const unsigned ublocks = (unsigned)std::min<int64_t>(cdiv(nupd, kThreads), 1024);
     hipLaunchKernelGGL(k_update, dim3(ublocks), dim3(kThreads), 0, c->stream, c->p);
     LAUNCH_CHECK("k_update");
-    ev_record(c, timed_it, 7);
+    ev_record(c, it, 6, 1);
     return 0;
 }
 
@@ -327,6 +340,8 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     p.g = (double*)(s + L.g);
     p.D = (double*)(s + L.D);
     p.parts = (double*)(s + L.parts);
+    p.parts2 = (double*)(s + L.parts2);
+    p.reverse_rows = c->reverse_rows;
     p.comm = (double*)(s + L.comm);
     p.r = (double*)(s + L.r);
     p.Ax = (double*)(s + L.Ax);
@@ -517,6 +532,18 @@ int bpgl_iterate(bpgl_ctx* c, int64_t n_iter, const int32_t* order, double mu, c
     return 0;
 }
 
+int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
+    if (!c || !key) return fail(BPGL_E_ARG, "null argument");
+    if (!strcmp(key, "reverse_rows")) {
+        c->reverse_rows = value != 0;
+        c->p.reverse_rows = c->reverse_rows;
+        if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+        c->solver = false;   // a new bpgl_solver_reset re-captures the iteration
+        return 0;
+    }
+    return fail(BPGL_E_ARG, "unknown tuning key '%s'", key);
+}
+
 int bpgl_set_kernel_timing(bpgl_ctx* c, int enable) {
     if (!c) return fail(BPGL_E_ARG, "null context");
     c->timing = enable != 0;
@@ -528,12 +555,14 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     if (!c || !avg_ms) return fail(BPGL_E_ARG, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    // kinds: 0 colpass, 1 shrink, 2 rowpass, 3 rowreduce, 4 allreduce, 5 step, 6 update
     double sum[kTimedKinds] = {0};
+    const bool multi = c->comm != nullptr;
     for (int64_t it = 0; it < c->timed_iters; ++it) {
         for (int k = 0; k < kTimedKinds; ++k) {
+            if (!multi && (k == 4 || k == 5)) continue;
             float ms = 0.f;
-            const size_t i0 = (size_t)it * (kTimedKinds + 1) + k;
+            const size_t i0 = 2 * ((size_t)it * kTimedKinds + k);
+            if (i0 + 1 >= c->evs.size()) continue;
             HIP_TRY(hipEventElapsedTime(&ms, c->evs[i0], c->evs[i0 + 1]));
             sum[k] += ms;
         }

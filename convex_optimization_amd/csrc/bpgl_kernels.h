@@ -37,7 +37,8 @@ struct DevState {
     double err;           // error criterion of the last iteration
     double r1, r2;        // line-search numerators (diagnostics)
     long long iters;      // iterations completed (update applied or stop reached)
-    long long pad[5];
+    unsigned long long cnt_rowreduce;   // monotonic arrival counter of k_rowreduce blocks
+    long long pad[4];
 };
 
 struct Params {
@@ -50,7 +51,9 @@ struct Params {
     double* slab_s;   // [nseg][m]
     double* g;        // [wp]
     double* D;        // [wp]
-    double* parts;    // [nparts][4]
+    double* parts;    // [nparts][4]   shrink partials (sum |Bx|, sum |x|, max err)
+    double* parts2;   // [m/64][2]     rowreduce partials (sum r s23, sum s23^2)
+    int reverse_rows;  // rowpass walks row chunks last-to-first (Infinity Cache reuse)
     double* comm;     // [m + 2 + nranks]
     double* r;        // [m]   residual s11 = sum_k Ax_k - b
     double* Ax;       // [nblock][m]
@@ -235,14 +238,36 @@ __device__ __forceinline__ double proj(double v, double lo, double hi) {  // cpu
     return a > lo ? a : lo;
 }
 
+// block = 64 columns x 4 waves: wave q sums row chunks q, q+4, ... of the slab
+// for its 64 columns, the 4 wave sums are added in a fixed order, wave 0 runs
+// the best-response epilogue.  grid = nparts = w_pad / 64.
+constexpr int kColsPerShrink = 64;
 __global__ __launch_bounds__(kThreads) void k_shrink(Params p) {
     if (p.st->done) return;
     const int mb = cur_block(p);
-    const long long j = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long j = (long long)blockIdx.x * kColsPerShrink + lane;
+    const long long jj = j < p.wp ? j : p.wp - 1;
+    double acc = 0.0;
+    {
+        int c = wave;
+#pragma unroll 4
+        for (; c + 3 * kWaves < p.nchunk; c += 4 * kWaves) {
+            const double a0 = p.slab_g[(long long)c * p.wp + jj];
+            const double a1 = p.slab_g[(long long)(c + kWaves) * p.wp + jj];
+            const double a2 = p.slab_g[(long long)(c + 2 * kWaves) * p.wp + jj];
+            const double a3 = p.slab_g[(long long)(c + 3 * kWaves) * p.wp + jj];
+            acc = (((acc + a0) + a1) + a2) + a3;
+        }
+        for (; c < p.nchunk; c += kWaves) acc += p.slab_g[(long long)c * p.wp + jj];
+    }
+    __shared__ double red[kWaves][64];
+    red[wave][lane] = acc;
+    __syncthreads();
+    if (wave != 0) return;
     double abx = 0.0, ax = 0.0, err = 0.0;
     if (j < p.wp) {
-        double g = 0.0;
-        for (int c = 0; c < p.nchunk; ++c) g += p.slab_g[(long long)c * p.wp + j];
+        const double g = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
         p.g[j] = g;
         double Dj = 0.0;
         if (j < p.w) {
@@ -257,21 +282,12 @@ __global__ __launch_bounds__(kThreads) void k_shrink(Params p) {
         }
         p.D[j] = Dj;
     }
-    // block reduction (fixed order): wave shuffles then 4 wave results
-    __shared__ double sred[3][kWaves];
     abx = wave_sum(abx);
     ax = wave_sum(ax);
     err = wave_max(err);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) { sred[0][wave] = abx; sred[1][wave] = ax; sred[2][wave] = err; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
-        double b = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
-        double e = sred[2][0];
-        for (int q = 1; q < kWaves; ++q) e = (sred[2][q] > e || sred[2][q] != sred[2][q]) ? sred[2][q] : e;
+    if (lane == 0) {
         double* dst = p.parts + 4ll * blockIdx.x;
-        dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
+        dst[0] = abx; dst[1] = ax; dst[2] = err; dst[3] = 0.0;
     }
 }
 
@@ -290,7 +306,8 @@ __global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __
     if (fixed_block < 0 && p.st->done) return;
     const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
     const int seg = blockIdx.x % p.nseg;
-    const int chunk = blockIdx.x / p.nseg;
+    const int chunk0 = blockIdx.x / p.nseg;
+    const int chunk = p.reverse_rows ? p.nchunk - 1 - chunk0 : chunk0;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
@@ -357,47 +374,158 @@ __global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __
 }
 
 // ---------------------------------------------------------------------------
-// rowreduce: out[i] = sum_{q < nseg} slab_s[q][i]; with `solver` set, block 0
-// also folds the shrink partials into out[m], out[m+1], out[m+2+rank].
+// line search + stopping rule on fully reduced scalars (lasso.py:129-150)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* __restrict__ slab,
-                                                        double* __restrict__ out, int solver) {
-    if (solver && p.st->done) return;
-    const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
-    if (i < p.m) {
-        double s = 0.0;
-        for (int q = 0; q < p.nseg; ++q) s += slab[(long long)q * p.m + i];
-        out[i] = s;
-    }
-    if (solver && blockIdx.x == 0) {
-        __shared__ double sred[3][kWaves];
-        double a = 0.0, b = 0.0, e = 0.0;
-        for (int k = threadIdx.x; k < p.nparts; k += kThreads) {
-            a += p.parts[4ll * k];
-            b += p.parts[4ll * k + 1];
-            const double ek = p.parts[4ll * k + 2];
-            e = (ek > e || ek != ek) ? ek : e;
-        }
-        a = wave_sum(a);
-        b = wave_sum(b);
-        e = wave_max(e);
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        if (lane == 0) { sred[0][wave] = a; sred[1][wave] = b; sred[2][wave] = e; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            a = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
-            b = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
-            e = sred[2][0];
-            for (int q = 1; q < kWaves; ++q) e = (sred[2][q] > e || sred[2][q] != sred[2][q]) ? sred[2][q] : e;
-            out[p.m] = a;
-            out[p.m + 1] = b;
-            for (int r = 0; r < p.nranks; ++r) out[p.m + 2 + r] = (r == p.rank) ? e : 0.0;
+__device__ void finish_step(const Params& p, double rs, double ss, double l1bx, double l1x, double err) {
+    const double r1 = rs + p.mu * (l1bx - l1x);           // lasso.py:129-131
+    const double r2 = ss;                                 // lasso.py:132
+    const double gamma = (r2 == 0.0) ? 0.0 : proj(-r1 / r2, 0.0, 1.0);   // lasso.py:133-136
+    DevState* st = p.st;
+    const long long t = st->t;
+    const int mb = cur_block(p);
+    if (p.err_iter && t < p.rec_len) p.err_iter[t] = err;
+    st->r1 = r1;
+    st->r2 = r2;
+    st->err = err;
+    st->t_last = t;
+    st->cur_mb = mb;
+    if (p.err_bound >= 0.0) {                             // lasso.py:141-150
+        if (err < p.err_bound) st->block_cnt += 1;
+        if (mb == p.nblock - 1) {
+            if (st->block_cnt == p.nblock) {
+                st->done = 1;
+                st->gamma = 0.0;
+                st->iters = t + 1;
+                return;
+            }
+            st->block_cnt = 0;
         }
     }
+    st->gamma = gamma;
+    st->t = t + 1;
+}
+
+// fold the shrink partials (fixed order) : sum |Bx|, sum |x|, max err
+__device__ void fold_parts(const Params& p, double& a, double& b, double& e) {
+    __shared__ double sred[3][kWaves];
+    a = 0.0; b = 0.0; e = 0.0;
+    for (int k = threadIdx.x; k < p.nparts; k += kThreads) {
+        a += p.parts[4ll * k];
+        b += p.parts[4ll * k + 1];
+        const double ek = p.parts[4ll * k + 2];
+        e = (ek > e || ek != ek) ? ek : e;
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    e = wave_max(e);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { sred[0][wave] = a; sred[1][wave] = b; sred[2][wave] = e; }
+    __syncthreads();
+    a = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
+    b = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
+    e = sred[2][0];
+    for (int q = 1; q < kWaves; ++q) e = (sred[2][q] > e || sred[2][q] != sred[2][q]) ? sred[2][q] : e;
+}
+
+__device__ __forceinline__ void st_agent(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 // ---------------------------------------------------------------------------
-// step: exact line search (lasso.py:129-136) + stopping rule (lasso.py:141-150)
+// rowreduce: out[i] = sum_{q < nseg} slab_s[q][i]  (block = 64 rows x 4 waves,
+// wave q sums segments q, q+4, ...; fixed-order combine).
+//   mode 0 : plain reduction (bpgl_mv API)
+//   mode 1 : solver, single rank: per-block partials of r.s23 and s23.s23, and
+//            the LAST arriving block (agent-scope counter, write-through
+//            partials) folds all partials and runs the line search.
+//   mode 2 : solver, multi rank: out = this rank's partial s23; block 0 adds
+//            [sum |Bx|, sum |x|, err slot] for the all-reduce; k_step follows.
+// ---------------------------------------------------------------------------
+constexpr int kRowsPerReduce = 64;
+__global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* __restrict__ slab,
+                                                        double* __restrict__ out, int mode) {
+    if (mode && p.st->done) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long i = (long long)blockIdx.x * kRowsPerReduce + lane;
+    const long long ii = i < p.m ? i : p.m - 1;
+    double acc = 0.0;
+    {
+        int q = wave;
+#pragma unroll 4
+        for (; q + 3 * kWaves < p.nseg; q += 4 * kWaves) {
+            const double a0 = slab[(long long)q * p.m + ii];
+            const double a1 = slab[(long long)(q + kWaves) * p.m + ii];
+            const double a2 = slab[(long long)(q + 2 * kWaves) * p.m + ii];
+            const double a3 = slab[(long long)(q + 3 * kWaves) * p.m + ii];
+            acc = (((acc + a0) + a1) + a2) + a3;
+        }
+        for (; q < p.nseg; q += kWaves) acc += slab[(long long)q * p.m + ii];
+    }
+    __shared__ double red[kWaves][64];
+    __shared__ int am_last;
+    red[wave][lane] = acc;
+    __syncthreads();
+    double s = 0.0;
+    if (wave == 0 && i < p.m) {
+        s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+        out[i] = s;
+    }
+    if (mode == 2) {
+        if (blockIdx.x == 0) {
+            double a, b, e;
+            fold_parts(p, a, b, e);
+            if (threadIdx.x == 0) {
+                out[p.m] = a;
+                out[p.m + 1] = b;
+                for (int r = 0; r < p.nranks; ++r) out[p.m + 2 + r] = (r == p.rank) ? e : 0.0;
+            }
+        }
+        return;
+    }
+    if (mode != 1) return;
+    if (wave == 0) {
+        double rs = (i < p.m) ? p.r[i] * s : 0.0;
+        double ss = s * s;
+        rs = wave_sum(rs);
+        ss = wave_sum(ss);
+        if (lane == 0) {
+            st_agent(p.parts2 + 2ll * blockIdx.x, rs);
+            st_agent(p.parts2 + 2ll * blockIdx.x + 1, ss);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned long long old = __hip_atomic_fetch_add(&p.st->cnt_rowreduce, 1ull, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+            am_last = ((old + 1) % gridDim.x) == 0;
+        }
+    }
+    __syncthreads();
+    if (!am_last) return;
+    // last arriver: every other block's partials are visible (sc1 stores drained before its add)
+    double rs = 0.0, ss = 0.0;
+    {
+        __shared__ double sr[kWaves], sq[kWaves];
+        for (int k = threadIdx.x; k < (int)gridDim.x; k += kThreads) {
+            rs += ld_agent(p.parts2 + 2ll * k);
+            ss += ld_agent(p.parts2 + 2ll * k + 1);
+        }
+        rs = wave_sum(rs);
+        ss = wave_sum(ss);
+        if (lane == 0) { sr[wave] = rs; sq[wave] = ss; }
+        __syncthreads();
+        rs = ((sr[0] + sr[1]) + sr[2]) + sr[3];
+        ss = ((sq[0] + sq[1]) + sq[2]) + sq[3];
+    }
+    double a, b, e;
+    fold_parts(p, a, b, e);
+    if (threadIdx.x == 0) finish_step(p, rs, ss, a, b, e);
+}
+
+// ---------------------------------------------------------------------------
+// step (multi rank): after the all-reduce of [s23 | sum|Bx| | sum|x| | err slots]
 // one block of 1024 threads; fixed-order reductions.
 // ---------------------------------------------------------------------------
 constexpr int kStepThreads = 1024;
@@ -417,38 +545,14 @@ __global__ __launch_bounds__(kStepThreads) void k_step(Params p) {
     if (lane == 0) { sa[wave] = a; sb[wave] = b; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double r1 = 0.0, r2 = 0.0;
-        for (int q = 0; q < kStepThreads / 64; ++q) { r1 += sa[q]; r2 += sb[q]; }
-        r1 += p.mu * (s23[p.m] - s23[p.m + 1]);             // mu (||Bx||_1 - ||x_m||_1)
+        double rs = 0.0, ss = 0.0;
+        for (int q = 0; q < kStepThreads / 64; ++q) { rs += sa[q]; ss += sb[q]; }
         double err = s23[p.m + 2];
         for (int r = 1; r < p.nranks; ++r) {
             const double e = s23[p.m + 2 + r];
             err = (e > err || e != e) ? e : err;
         }
-        double gamma = (r2 == 0.0) ? 0.0 : proj(-r1 / r2, 0.0, 1.0);
-        DevState* st = p.st;
-        const long long t = st->t;
-        const int mb = cur_block(p);
-        if (p.err_iter && t < p.rec_len) p.err_iter[t] = err;
-        st->r1 = r1;
-        st->r2 = r2;
-        st->err = err;
-        st->t_last = t;
-        st->cur_mb = mb;
-        if (p.err_bound >= 0.0) {
-            if (err < p.err_bound) st->block_cnt += 1;
-            if (mb == p.nblock - 1) {
-                if (st->block_cnt == p.nblock) {
-                    st->done = 1;
-                    st->gamma = 0.0;
-                    st->iters = t + 1;
-                    return;
-                }
-                st->block_cnt = 0;
-            }
-        }
-        st->gamma = gamma;
-        st->t = t + 1;
+        finish_step(p, rs, ss, s23[p.m], s23[p.m + 1], err);
     }
 }
 

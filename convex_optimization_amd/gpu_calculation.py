@@ -28,6 +28,7 @@ Every compute call goes through libbpgl.so (``_native``); there is no
 alternative path.  Multi-GPU: pass ``comm=`` (see ``distributed.RankComm``);
 A is then this rank's column shard of every feature block.
 """
+import contextlib
 import ctypes
 
 import numpy as np
@@ -85,6 +86,7 @@ class GPU_Calculation:
                               ctypes.c_void_p(self.stream.cuda_stream)), "bpgl_create")
         self._ctx = ctx
         assert L.bpgl_block_width_padded(ctx) == Wp
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             At = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))
             if (At.is_cuda and At.dtype == tdt and At.is_contiguous() and Wp == W
@@ -164,7 +166,7 @@ class GPU_Calculation:
     def mat_tMulVec_DiffSize(self, s13, index_m, s11):
         """s13 <- A_m^T s11 (gpu_calculation.py:264-277)."""
         m = self._block_index(index_m)
-        with torch.cuda.stream(self.stream):
+        with self._on_stream():
             self._stage_in(s11, self._vin_h, self.MAT_HEIGHT)
             N.check(N.lib().bpgl_mtv(self._ctx, m, N.ptr(self._vin_h), N.ptr(self._vout_w)), "bpgl_mtv")
             self._stage_out(self._vout_w[:self.MAT_WIDTH], s13)
@@ -172,10 +174,21 @@ class GPU_Calculation:
     def matMulVec_DiffSize(self, s23, index_m, descent_d):
         """s23 <- A_m descent_d (gpu_calculation.py:280-292)."""
         m = self._block_index(index_m)
-        with torch.cuda.stream(self.stream):
+        with self._on_stream():
             self._stage_in(descent_d, self._vin_w, self.MAT_WIDTH)
             N.check(N.lib().bpgl_mv(self._ctx, m, N.ptr(self._vin_w), N.ptr(self._vout_h)), "bpgl_mv")
             self._stage_out(self._vout_h, s23)
+
+    @contextlib.contextmanager
+    def _on_stream(self):
+        """Run on the library's stream, ordered after the caller's current stream and
+        before anything the caller enqueues afterwards (so device tensors produced or
+        consumed on torch's current stream are race-free)."""
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            yield
+        cur.wait_stream(self.stream)
 
     def _block_index(self, index_m):
         m = int(index_m)
@@ -188,7 +201,7 @@ class GPU_Calculation:
         """Prepare a device-resident run.  ``order``: None (cyclic) or a sequence of block indices."""
         L = N.lib()
         H, W, Wp, B = self.MAT_HEIGHT, self.MAT_WIDTH, self.MAT_WIDTH_PAD, self.Block
-        with torch.cuda.stream(self.stream):
+        with self._on_stream():
             self._b = torch.empty(H, dtype=torch.float64, device=self.device)
             self._stage_in(b, self._b, H)
             self._x = torch.zeros((B, Wp), dtype=torch.float64, device=self.device)
@@ -215,7 +228,8 @@ class GPU_Calculation:
                 "bpgl_solver_reset")
 
     def solver_step(self, n_iter):
-        N.check(N.lib().bpgl_solver_step(self._ctx, int(n_iter)), "bpgl_solver_step")
+        with self._on_stream():
+            N.check(N.lib().bpgl_solver_step(self._ctx, int(n_iter)), "bpgl_solver_step")
 
     def solver_status(self):
         it, st, tl = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int64()
@@ -243,6 +257,9 @@ class GPU_Calculation:
         if self._err_iter is None:
             return None, None
         return self._err_iter.cpu().numpy().copy(), self._time_iter.cpu().numpy().copy()
+
+    def set_tuning(self, key, value):
+        N.check(N.lib().bpgl_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_set_tuning")
 
     def set_kernel_timing(self, enable):
         N.check(N.lib().bpgl_set_kernel_timing(self._ctx, int(bool(enable))), "bpgl_set_kernel_timing")

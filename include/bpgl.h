@@ -146,10 +146,17 @@ int bpgl_iterate(bpgl_ctx* ctx, int64_t n_iter, const int32_t* order, double mu,
 /* Timing of the most recent bpgl_solver_step window on the context stream:
  * average duration (ms) of each kernel kind over the window, measured with
  * HIP events when profiling was enabled by bpgl_set_kernel_timing(ctx, 1).
- * kinds: 0 colpass (A^T r), 1 shrink, 2 rowpass (A D), 3 rowreduce, 4 step,
- * 5 update, 6 allreduce. */
+ * kinds: 0 colpass (A^T r), 1 shrink, 2 rowpass (A D), 3 rowreduce (+ line
+ * search on one rank), 4 allreduce, 5 step (multi-rank line search), 6 update. */
 int bpgl_set_kernel_timing(bpgl_ctx* ctx, int enable);
 int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 7 */, int64_t* samples);
+
+/* Runtime tuning knobs (call before bpgl_solver_reset):
+ *   "reverse_rows" (default 1): the A D pass walks row chunks last-to-first so
+ *   its first reads hit the Infinity Cache lines the A^T r pass read last.
+ * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the
+ * number of (row chunk x column segment) tiles per pass (default 2048). */
+int bpgl_set_tuning(bpgl_ctx* ctx, const char* key, int64_t value);
 
 /* Launch geometry chosen for this context (diagnostics). */
 int bpgl_geometry(const bpgl_ctx* ctx, int32_t* nseg, int32_t* nchunk, int32_t* rows_per_chunk,
