@@ -48,6 +48,9 @@ _SIGS = {
     "bpgl_mv": (_int, [_p, _i32, _p, _p]),
     "bpgl_comm_unique_id": (_int, [_p]),
     "bpgl_comm_init": (_int, [_p, _p, _int, _int]),
+    "bpgl_set_ranks": (_int, [_p, _int, _int]),
+    "bpgl_solver_phase": (_int, [_p, _int]),
+    "bpgl_solver_exchange_buffer": (_p, [_p, ctypes.POINTER(_i64)]),
     "bpgl_solver_reset": (_int, [_p, _p, _f64, _p, _p, _i64, _f64, _p, _p, _i64, _int]),
     "bpgl_solver_step": (_int, [_p, _i64]),
     "bpgl_solver_status": (_int, [_p, ctypes.POINTER(_i64), ctypes.POINTER(_int), ctypes.POINTER(_i64),

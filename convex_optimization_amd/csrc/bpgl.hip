@@ -72,6 +72,7 @@ struct bpgl_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
+    bool external = false;   // nranks > 1 with the exchange done by the caller
     // solver
     bool solver = false, use_graph = false;
     hipGraphExec_t gexec = nullptr;
@@ -80,7 +81,9 @@ struct bpgl_ctx {
     std::vector<hipEvent_t> evs;   // (kinds + 1) events per timed iteration
     int64_t timed_iters = 0;
     double wall_tick_s = 1e-8;
-    int reverse_rows = 1;
+    int reverse_rows = 0;
+    int nt_loads = 1;
+    int tail_permille = 120;
 };
 
 namespace {
@@ -91,7 +94,7 @@ void geometry(bpgl_ctx* c) {
     c->wp = up(c->w, V);
     c->nseg = (int)cdiv(c->wp, c->segw);
     // ~8 blocks per CU on 256 CUs, rows per chunk a multiple of 16 (4 waves x 4 rows)
-    int64_t target = 2048;
+    int64_t target = 1024;
     if (const char* e = getenv("BPGL_TARGET_BLOCKS")) target = std::max<int64_t>(1, atoll(e));
     int64_t nchunk = std::max<int64_t>(1, cdiv(target, c->nseg));
     nchunk = std::min<int64_t>(nchunk, cdiv(c->m, 16));
@@ -137,10 +140,12 @@ dim3 grid_tiles(const bpgl_ctx* c) { return dim3((unsigned)((int64_t)c->nseg * c
 
 template <typename T>
 int launch_colpass(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_block) {
-    if (mode == 0)
-        hipLaunchKernelGGL((k_colpass<T, 0>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+    if (mode == 0 && c->nt_loads)
+        hipLaunchKernelGGL((k_colpass<T, 0, true>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+    else if (mode == 0)
+        hipLaunchKernelGGL((k_colpass<T, 0, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
     else
-        hipLaunchKernelGGL((k_colpass<T, 1>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+        hipLaunchKernelGGL((k_colpass<T, 1, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
     LAUNCH_CHECK("k_colpass");
     return 0;
 }
@@ -153,7 +158,10 @@ int colpass(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_bl
 }
 template <typename T>
 int launch_rowpass(bpgl_ctx* c, const double* d, double* slab, int fixed_block) {
-    hipLaunchKernelGGL((k_rowpass<T>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, d, slab, fixed_block);
+    if (c->nt_loads)
+        hipLaunchKernelGGL((k_rowpass<T, true>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, d, slab, fixed_block);
+    else
+        hipLaunchKernelGGL((k_rowpass<T, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, d, slab, fixed_block);
     LAUNCH_CHECK("k_rowpass");
     return 0;
 }
@@ -194,40 +202,58 @@ void ev_record(bpgl_ctx* c, int64_t it, int kind, int end) {
 // One block update, enqueued on c->stream.  The block index and every
 // iteration-dependent value are read on the device from the state words, so
 // the same launch sequence (or its captured graph) serves every iteration.
-int enqueue_iteration(bpgl_ctx* c, int64_t it) {
+// phase 0: colpass, shrink, rowpass, rowreduce [, allreduce, step]; phase 1: update.
+// With the caller doing the exchange (external ranks) phase 0 stops after
+// rowreduce and phase 1 starts with the step.
+int enqueue_phase(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
-    const bool multi = c->comm != nullptr;
-    ev_record(c, it, 0, 0);
-    if ((rc = colpass(c, 0, c->p.r, c->p.slab_g, -1))) return rc;
-    ev_record(c, it, 0, 1);
-    ev_record(c, it, 1, 0);
-    hipLaunchKernelGGL(k_shrink, dim3((unsigned)c->nparts), dim3(kThreads), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_shrink");
-    ev_record(c, it, 1, 1);
-    ev_record(c, it, 2, 0);
-    if ((rc = rowpass(c, c->p.D, c->p.slab_s, -1))) return rc;
-    ev_record(c, it, 2, 1);
-    ev_record(c, it, 3, 0);
-    if ((rc = rowreduce(c, c->p.slab_s, c->p.comm, multi ? 2 : 1))) return rc;
-    ev_record(c, it, 3, 1);
-    if (multi) {
-        ev_record(c, it, 4, 0);
-        ncclResult_t nr = ncclAllReduce(c->p.comm, c->p.comm, (size_t)(c->m + 2 + c->nranks), ncclFloat64,
-                                        ncclSum, c->comm, c->stream);
-        if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
-        ev_record(c, it, 4, 1);
+    const bool multi = c->comm != nullptr || c->external;
+    if (phase == 0) {
+        ev_record(c, it, 0, 0);
+        if ((rc = colpass(c, 0, c->p.r, c->p.slab_g, -1))) return rc;
+        ev_record(c, it, 0, 1);
+        ev_record(c, it, 1, 0);
+        hipLaunchKernelGGL(k_shrink, dim3((unsigned)c->nparts), dim3(kThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_shrink");
+        ev_record(c, it, 1, 1);
+        ev_record(c, it, 2, 0);
+        if ((rc = rowpass(c, c->p.D, c->p.slab_s, -1))) return rc;
+        ev_record(c, it, 2, 1);
+        ev_record(c, it, 3, 0);
+        if ((rc = rowreduce(c, c->p.slab_s, c->p.comm, multi ? 2 : 1))) return rc;
+        ev_record(c, it, 3, 1);
+        if (c->comm) {
+            ev_record(c, it, 4, 0);
+            ncclResult_t nr = ncclAllReduce(c->p.comm, c->p.comm, (size_t)(c->m + 2 + c->nranks), ncclFloat64,
+                                            ncclSum, c->comm, c->stream);
+            if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
+            ev_record(c, it, 4, 1);
+        }
+    }
+    if ((phase == 0 && c->comm) || (phase == 1 && c->external)) {
         ev_record(c, it, 5, 0);
         hipLaunchKernelGGL(k_step, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
         LAUNCH_CHECK("k_step");
         ev_record(c, it, 5, 1);
     }
-    ev_record(c, it, 6, 0);
-    const int64_t nupd = std::max<int64_t>(c->wp, c->m);
-    const unsigned ublocks = (unsigned)std::min<int64_t>(cdiv(nupd, kThreads), 1024);
-    hipLaunchKernelGGL(k_update, dim3(ublocks), dim3(kThreads), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_update");
-    ev_record(c, it, 6, 1);
+    if (phase == 1) {
+        ev_record(c, it, 6, 0);
+        const int64_t nupd = std::max<int64_t>(c->wp, c->m);
+        const unsigned ublocks = (unsigned)std::min<int64_t>(cdiv(nupd, kThreads), 1024);
+        hipLaunchKernelGGL(k_update, dim3(ublocks), dim3(kThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_update");
+        ev_record(c, it, 6, 1);
+    }
     return 0;
+}
+
+// One block update, enqueued on c->stream.  The block index and every
+// iteration-dependent value are read on the device from the state words, so
+// the same launch sequence (or its captured graph) serves every iteration.
+int enqueue_iteration(bpgl_ctx* c, int64_t it) {
+    int rc;
+    if ((rc = enqueue_phase(c, it, 0))) return rc;
+    return enqueue_phase(c, it, 1);
 }
 
 }  // namespace
@@ -342,6 +368,7 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     p.parts = (double*)(s + L.parts);
     p.parts2 = (double*)(s + L.parts2);
     p.reverse_rows = c->reverse_rows;
+    p.tail_permille = c->tail_permille;
     p.comm = (double*)(s + L.comm);
     p.r = (double*)(s + L.r);
     p.Ax = (double*)(s + L.Ax);
@@ -427,8 +454,40 @@ int bpgl_comm_init(bpgl_ctx* c, const void* uid, int rank, int nranks) {
         if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(nr));
     }
     c->p.has_comm = c->comm != nullptr;
+    c->external = false;
     if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
     return 0;
+}
+
+int bpgl_set_ranks(bpgl_ctx* c, int rank, int nranks) {
+    if (!c) return fail(BPGL_E_ARG, "null context");
+    if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
+        return fail(BPGL_E_ARG, "bad rank %d / nranks %d", rank, nranks);
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    c->rank = rank;
+    c->nranks = nranks;
+    c->p.rank = rank;
+    c->p.nranks = nranks;
+    c->p.has_comm = 0;
+    c->external = nranks > 1;
+    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    c->solver = false;
+    return 0;
+}
+
+int bpgl_solver_phase(bpgl_ctx* c, int phase) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    if (!c->solver) return fail(BPGL_E_STATE, "bpgl_solver_reset has not been called");
+    if (phase != 0 && phase != 1) return fail(BPGL_E_ARG, "phase must be 0 or 1");
+    HIP_TRY(hipSetDevice(c->device));
+    return enqueue_phase(c, 0, phase);
+}
+
+double* bpgl_solver_exchange_buffer(bpgl_ctx* c, int64_t* count) {
+    if (!c) return nullptr;
+    if (count) *count = c->m + 2 + c->nranks;
+    return c->p.comm;
 }
 
 int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const int32_t* order,
@@ -466,7 +525,7 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
                        c->stream, p);
     LAUNCH_CHECK("k_reset");
     if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-    c->use_graph = use_graph != 0;
+    c->use_graph = use_graph != 0 && !c->external;
     if (c->use_graph) {
         hipGraph_t graph = nullptr;
         const bool was_timing = c->timing;
@@ -491,6 +550,7 @@ int bpgl_solver_step(bpgl_ctx* c, int64_t n_iter) {
     if ((rc = check_ready(c))) return rc;
     if (!c->solver) return fail(BPGL_E_STATE, "bpgl_solver_reset has not been called");
     if (n_iter < 0) return fail(BPGL_E_ARG, "n_iter < 0");
+    if (c->external) return fail(BPGL_E_STATE, "external-exchange ranks advance with bpgl_solver_phase");
     HIP_TRY(hipSetDevice(c->device));
     for (int64_t i = 0; i < n_iter; ++i) {
         if (c->timing || !c->gexec) {
@@ -541,6 +601,20 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->solver = false;   // a new bpgl_solver_reset re-captures the iteration
         return 0;
     }
+    if (!strcmp(key, "tail_permille")) {
+        if (value < 0 || value > 1000) return fail(BPGL_E_ARG, "tail_permille must be in [0, 1000]");
+        c->tail_permille = (int)value;
+        c->p.tail_permille = c->tail_permille;
+        if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "nt_loads")) {
+        c->nt_loads = value != 0;
+        if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+        c->solver = false;
+        return 0;
+    }
     return fail(BPGL_E_ARG, "unknown tuning key '%s'", key);
 }
 
@@ -556,10 +630,11 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     double sum[kTimedKinds] = {0};
-    const bool multi = c->comm != nullptr;
+    const bool multi = c->comm != nullptr || c->external;
     for (int64_t it = 0; it < c->timed_iters; ++it) {
         for (int k = 0; k < kTimedKinds; ++k) {
             if (!multi && (k == 4 || k == 5)) continue;
+            if (!c->comm && k == 4) continue;
             float ms = 0.f;
             const size_t i0 = 2 * ((size_t)it * kTimedKinds + k);
             if (i0 + 1 >= c->evs.size()) continue;

@@ -53,7 +53,8 @@ struct Params {
     double* D;        // [wp]
     double* parts;    // [nparts][4]   shrink partials (sum |Bx|, sum |x|, max err)
     double* parts2;   // [m/64][2]     rowreduce partials (sum r s23, sum s23^2)
-    int reverse_rows;  // rowpass walks row chunks last-to-first (Infinity Cache reuse)
+    int reverse_rows;  // rowpass walks each chunk's rows bottom-up (Infinity Cache reuse)
+    int tail_permille; // with NT loads: share of each chunk read last with allocating loads
     double* comm;     // [m + 2 + nranks]
     double* r;        // [m]   residual s11 = sum_k Ax_k - b
     double* Ax;       // [nblock][m]
@@ -100,9 +101,19 @@ template <> struct VecT<bf16_t> {
     }
 };
 
-template <typename T>
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <typename T, bool NT = false>
 __device__ __forceinline__ typename VecT<T>::raw ldv(const T* p) {
-    return *reinterpret_cast<const typename VecT<T>::raw*>(p);
+    using raw = typename VecT<T>::raw;
+    if constexpr (NT) {
+        // non-temporal 16-byte load (streamed-once A)
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        raw o;
+        __builtin_memcpy(&o, &v, sizeof(raw));
+        return o;
+    } else {
+        return *reinterpret_cast<const raw*>(p);
+    }
 }
 
 __device__ __forceinline__ int cur_block(const Params& p) {
@@ -129,7 +140,46 @@ __device__ __forceinline__ double wave_max(double v) {
 // R rows; the 4 waves split the rows (wave q: rows q, q+4, ...) and sum their
 // fp64 partials through LDS in a fixed order.
 // ---------------------------------------------------------------------------
-template <typename T, int MODE>
+// rows [i, istop) of one wave (step 2 x 4 rows: rows i and i + 4 per trip)
+template <typename T, int MODE, bool NT>
+__device__ __forceinline__ void colpass_span(const T* __restrict__ Ab, long long lda, const long long (&col)[kU],
+                                             const double* __restrict__ vec, long long& i, long long istop,
+                                             long long i1, double (&acc)[kU][VecT<T>::N]) {
+    constexpr int V = VecT<T>::N;
+    using raw = typename VecT<T>::raw;
+    for (; i < istop; i += 2 * kWaves) {
+        const bool two = i + kWaves < i1;
+        const long long i2 = two ? i + kWaves : i;
+        const T* r0 = Ab + i * lda;
+        const T* r1 = Ab + i2 * lda;
+        raw a0[kU], a1[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) a0[u] = ldv<T, NT>(r0 + col[u]);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) a1[u] = ldv<T, NT>(r1 + col[u]);
+        double s0 = 1.0, s1 = 1.0;
+        if (MODE == 0) { s0 = vec[i]; s1 = vec[i2]; }   // i2 == i when !two: in bounds
+        s1 = two ? s1 : 0.0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            double v0[V], v1[V];
+            VecT<T>::cvt(a0[u], v0);
+            VecT<T>::cvt(a1[u], v1);
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                if (MODE == 0) {
+                    acc[u][e] = fma(v0[e], s0, acc[u][e]);
+                    acc[u][e] = fma(v1[e], s1, acc[u][e]);
+                } else {
+                    acc[u][e] = fma(v0[e], v0[e], acc[u][e]);
+                    acc[u][e] = fma(v1[e] * s1, v1[e], acc[u][e]);
+                }
+            }
+        }
+    }
+}
+
+template <typename T, int MODE, bool NT>
 __global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __restrict__ vec,
                                                       double* __restrict__ slab, int fixed_block) {
     constexpr int V = VecT<T>::N;
@@ -159,36 +209,15 @@ __global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __
 
     const long long i0 = (long long)chunk * p.R;
     const long long i1 = (i0 + p.R < p.m) ? i0 + p.R : p.m;
-    for (long long i = i0 + wave; i < i1; i += 2 * kWaves) {
-        const bool two = i + kWaves < i1;
-        const long long i2 = two ? i + kWaves : i;
-        const T* r0 = Ab + i * p.lda;
-        const T* r1 = Ab + i2 * p.lda;
-        raw a0[kU], a1[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) a0[u] = ldv<T>(r0 + col[u]);
-#pragma unroll
-        for (int u = 0; u < kU; ++u) a1[u] = ldv<T>(r1 + col[u]);
-        double s0 = 1.0, s1 = 1.0;
-        if (MODE == 0) { s0 = vec[i]; s1 = vec[i2]; }   // i2 == i when !two: in bounds
-        s1 = two ? s1 : 0.0;
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            double v0[V], v1[V];
-            VecT<T>::cvt(a0[u], v0);
-            VecT<T>::cvt(a1[u], v1);
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                if (MODE == 0) {
-                    acc[u][e] = fma(v0[e], s0, acc[u][e]);
-                    acc[u][e] = fma(v1[e], s1, acc[u][e]);
-                } else {
-                    acc[u][e] = fma(v0[e], v0[e], acc[u][e]);
-                    acc[u][e] = fma(v1[e] * s1, v1[e], acc[u][e]);
-                }
-            }
-        }
+    // the rows this wave reads last (the bottom `tail` of the chunk) use plain,
+    // cache-allocating loads: k_rowpass reads them first.  Everything else is
+    // a non-temporal stream.
+    long long i = i0 + wave;
+    if (NT) {
+        const long long isplit = i1 - ((i1 - i0) * p.tail_permille) / 1000;
+        colpass_span<T, MODE, true>(Ab, p.lda, col, vec, i, isplit, i1, acc);
     }
+    colpass_span<T, MODE, false>(Ab, p.lda, col, vec, i, i1, i1, acc);
     // cross-wave reduction in a fixed order (wave 0 + 1 + 2 + 3)
     __shared__ double red[kWaves][kU * V][64];
 #pragma unroll
@@ -297,7 +326,58 @@ __global__ __launch_bounds__(kThreads) void k_shrink(Params p) {
 // four per-lane partials are reduced with a transposed butterfly (7 fp64
 // shuffles per 4 rows instead of 24): lanes 0/16/32/48 end with rows 0..3.
 // ---------------------------------------------------------------------------
-template <typename T>
+// one 16-row group of k_rowpass: rows ib, ib+4, ib+8, ib+12 of this wave
+template <typename T, bool NT>
+__device__ __forceinline__ void rowpass_group(const T* __restrict__ Ab, long long lda, const long long (&col)[kU],
+                                          const double (&dv)[kU][VecT<T>::N], long long ib, long long i1,
+                                          double* __restrict__ out, int lane) {
+    constexpr int V = VecT<T>::N;
+    using raw = typename VecT<T>::raw;
+    long long rows[4];
+    const T* rp[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        rows[k] = ib + k * kWaves;
+        rp[k] = Ab + (rows[k] < i1 ? rows[k] : ib) * lda;
+    }
+    raw a[4][kU];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) a[k][u] = ldv<T, NT>(rp[k] + col[u]);
+    double ps[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            double v[V];
+            VecT<T>::cvt(a[k][u], v);
+#pragma unroll
+            for (int e = 0; e < V; ++e) s = fma(v[e], dv[u][e], s);
+        }
+        ps[k] = s;
+    }
+    // transposed butterfly over the 64 lanes
+    const bool up = lane & 32;
+    const double k0 = up ? ps[2] : ps[0], k1 = up ? ps[3] : ps[1];
+    const double s0 = up ? ps[0] : ps[2], s1 = up ? ps[1] : ps[3];
+    const double q0 = k0 + __shfl_xor(s0, 32);
+    const double q1 = k1 + __shfl_xor(s1, 32);
+    const bool hb = lane & 16;
+    double v = (hb ? q1 : q0) + __shfl_xor(hb ? q0 : q1, 16);
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 1);
+    if ((lane & 15) == 0) {
+        const int k = (up ? 2 : 0) + (hb ? 1 : 0);
+        const long long row = ib + k * kWaves;
+        if (row < i1) out[row] = v;
+    }
+}
+
+template <typename T, bool NT>
 __global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __restrict__ d,
                                                       double* __restrict__ slab, int fixed_block) {
     constexpr int V = VecT<T>::N;
@@ -306,8 +386,7 @@ __global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __
     if (fixed_block < 0 && p.st->done) return;
     const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
     const int seg = blockIdx.x % p.nseg;
-    const int chunk0 = blockIdx.x / p.nseg;
-    const int chunk = p.reverse_rows ? p.nchunk - 1 - chunk0 : chunk0;
+    const int chunk = blockIdx.x / p.nseg;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
@@ -327,49 +406,20 @@ __global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __
     const long long i0 = (long long)chunk * p.R;
     const long long i1 = (i0 + p.R < p.m) ? i0 + p.R : p.m;
     double* out = slab + (long long)seg * p.m;
-    for (long long ib = i0 + wave; ib < i1; ib += 4 * kWaves) {
-        long long rows[4];
-        const T* rp[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            rows[k] = ib + k * kWaves;
-            rp[k] = Ab + (rows[k] < i1 ? rows[k] : ib) * p.lda;
-        }
-        raw a[4][kU];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int u = 0; u < kU; ++u) a[k][u] = ldv<T>(rp[k] + col[u]);
-        double ps[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            double s = 0.0;
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                double v[V];
-                VecT<T>::cvt(a[k][u], v);
-#pragma unroll
-                for (int e = 0; e < V; ++e) s = fma(v[e], dv[u][e], s);
-            }
-            ps[k] = s;
-        }
-        // transposed butterfly over the 64 lanes
-        const bool up = lane & 32;
-        const double k0 = up ? ps[2] : ps[0], k1 = up ? ps[3] : ps[1];
-        const double s0 = up ? ps[0] : ps[2], s1 = up ? ps[1] : ps[3];
-        const double q0 = k0 + __shfl_xor(s0, 32);
-        const double q1 = k1 + __shfl_xor(s1, 32);
-        const bool hb = lane & 16;
-        double v = (hb ? q1 : q0) + __shfl_xor(hb ? q0 : q1, 16);
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 1);
-        if ((lane & 15) == 0) {
-            const int k = (up ? 2 : 0) + (hb ? 1 : 0);
-            const long long row = ib + k * kWaves;
-            if (row < i1) out[row] = v;
-        }
+    // reverse_rows: walk the chunk's 16-row groups bottom-up, so the first rows
+    // read are the ones k_colpass (top-down) read last with cache-allocating
+    // loads; the groups read last (the top `tail`) are loaded the same way for
+    // the next iteration's k_colpass.
+    const long long ngroups = (i1 - i0 + 4 * kWaves - 1) / (4 * kWaves);
+    const long long glate = NT ? ngroups - (ngroups * p.tail_permille) / 1000 : 0;
+    long long gi = 0;
+    for (; gi < glate; ++gi) {
+        const long long grp = p.reverse_rows ? ngroups - 1 - gi : gi;
+        rowpass_group<T, true>(Ab, p.lda, col, dv, i0 + grp * 4 * kWaves + wave, i1, out, lane);
+    }
+    for (; gi < ngroups; ++gi) {
+        const long long grp = p.reverse_rows ? ngroups - 1 - gi : gi;
+        rowpass_group<T, false>(Ab, p.lda, col, dv, i0 + grp * 4 * kWaves + wave, i1, out, lane);
     }
 }
 

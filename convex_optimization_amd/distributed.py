@@ -55,6 +55,18 @@ def assemble_x(x_shards, Block):
     return np.concatenate([np.concatenate([per[g][b] for g in range(nr)]) for b in range(Block)])
 
 
+def _rccl_unique_id():
+    from . import _native as N
+    buf = (ctypes.c_uint8 * 128)()
+    N.check(N.lib().bpgl_comm_unique_id(buf), "bpgl_comm_unique_id")
+    return bytes(buf)
+
+
+def exchange_layout(m, nranks):
+    """Offsets in the per-iteration all-reduce buffer (SUM over ranks)."""
+    return dict(s23=(0, m), l1_bx=m, l1_x=m + 1, err=(m + 2, m + 2 + nranks), count=m + 2 + nranks)
+
+
 class RankComm:
     """RCCL communicator of one rank, created inside libbpgl for a GPU_Calculation.
 
@@ -62,17 +74,18 @@ class RankComm:
     by bench.py and the CPU tests) used once to broadcast the unique id.
     """
 
-    def __init__(self, rank, world, group=None):
+    def __init__(self, rank, world, group=None, id_provider=None):
         self.rank, self.world, self.group = int(rank), int(world), group
+        self._id_provider = id_provider or _rccl_unique_id
 
     def unique_id(self):
+        """Rank 0 creates the 128-byte RCCL id; every rank returns the same bytes."""
         import torch
         import torch.distributed as dist
-        from . import _native as N
-        buf = (ctypes.c_uint8 * 128)()
-        if self.rank == 0:
-            N.check(N.lib().bpgl_comm_unique_id(buf), "bpgl_comm_unique_id")
-        t = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+        raw = self._id_provider() if self.rank == 0 else bytes(128)
+        if len(raw) != 128:
+            raise ValueError("an RCCL unique id is 128 bytes")
+        t = torch.tensor(list(raw), dtype=torch.uint8)
         if self.world > 1:
             dist.broadcast(t, src=0, group=self.group)
         return bytes(t.tolist())

@@ -258,6 +258,21 @@ class GPU_Calculation:
             return None, None
         return self._err_iter.cpu().numpy().copy(), self._time_iter.cpu().numpy().copy()
 
+    # -- caller-performed exchange (validation of the sharded kernels on one GPU) --
+    def set_ranks(self, rank, nranks):
+        N.check(N.lib().bpgl_set_ranks(self._ctx, int(rank), int(nranks)), "bpgl_set_ranks")
+
+    def solver_phase(self, phase):
+        with self._on_stream():
+            N.check(N.lib().bpgl_solver_phase(self._ctx, int(phase)), "bpgl_solver_phase")
+
+    def exchange_buffer(self):
+        """Device view of [s23 (m) | sum|Bx| | sum|x| | err slot per rank] (lives in the scratch)."""
+        cnt = ctypes.c_int64()
+        addr = N.lib().bpgl_solver_exchange_buffer(self._ctx, ctypes.byref(cnt))
+        off = (addr - self._scratch.data_ptr()) // 8
+        return self._scratch[off:off + cnt.value]
+
     def set_tuning(self, key, value):
         N.check(N.lib().bpgl_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_set_tuning")
 

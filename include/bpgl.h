@@ -111,6 +111,19 @@ int bpgl_comm_unique_id(void* out128);
 int bpgl_comm_init(bpgl_ctx* ctx, const void* unique_id128, int rank, int nranks);
 
 /*
+ * Caller-performed exchange (validation of the sharded kernels where RCCL
+ * cannot run, e.g. several ranks on one GPU): bpgl_set_ranks declares this
+ * context rank `rank` of `nranks` without a communicator.  Each iteration is
+ * then bpgl_solver_phase(ctx, 0); the caller sums the
+ * bpgl_solver_exchange_buffer (count = m + 2 + nranks fp64) over ranks and
+ * writes the sum back on every rank; bpgl_solver_phase(ctx, 1).  Requires the
+ * initial point x = 0.
+ */
+int bpgl_set_ranks(bpgl_ctx* ctx, int rank, int nranks);
+int bpgl_solver_phase(bpgl_ctx* ctx, int phase);
+double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
+
+/*
  * Device-resident solver (the loop of ClassLasso.run, lasso.py:190-292, and
  * ClassLassoCB_v2.run, lasso.py:458-613, with every step on the device).
  *
@@ -151,9 +164,12 @@ int bpgl_iterate(bpgl_ctx* ctx, int64_t n_iter, const int32_t* order, double mu,
 int bpgl_set_kernel_timing(bpgl_ctx* ctx, int enable);
 int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 7 */, int64_t* samples);
 
-/* Runtime tuning knobs (call before bpgl_solver_reset):
- *   "reverse_rows" (default 1): the A D pass walks row chunks last-to-first so
- *   its first reads hit the Infinity Cache lines the A^T r pass read last.
+/* Runtime tuning knobs (call before bpgl_solver_reset); none changes results:
+ *   "nt_loads" (default 1): stream A with non-temporal loads.
+ *   "tail_permille" (default 120): with nt_loads, the share of every row chunk
+ *   each pass reads last with cache-allocating loads (Infinity Cache reuse by
+ *   the other pass).
+ *   "reverse_rows" (default 0): the A D pass walks each row chunk bottom-up.
  * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the
  * number of (row chunk x column segment) tiles per pass (default 2048). */
 int bpgl_set_tuning(bpgl_ctx* ctx, const char* key, int64_t value);

@@ -121,7 +121,7 @@ def test_solver_matches_reference_run(golden, case, type_name):
     assert res["stopped"] == bool(fx["stopped"])
     assert rel(res["x"], x) <= 1e-9, rel(res["x"], x)
     T = int(fx["t_last"]) + 1
-    np.testing.assert_allclose(res["err_iter"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-12)
+    np.testing.assert_allclose(res["err_iter"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
     assert np.all(np.diff(res["time_iter"][:T]) >= 0)
 
 
@@ -221,3 +221,48 @@ def test_objective_monotone_at_full_size():
         objs.append(0.5 * float(torch.square(res).sum()) + mu * float(gc.solver_x_device().abs().sum()))
     assert all(b2 <= a2 * (1 + 1e-12) for a2, b2 in zip(objs, objs[1:])), objs
     assert objs[-1] < objs[0]
+
+
+# ---------------------------------------------------------------------------
+# column-sharded multi-rank kernels, with the all-reduce done by the test
+# (RCCL refuses two ranks on one GPU; the RCCL leg differs only by the call)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("case,world", [("c1_b2_p4_f32in", 2), ("c1_b1_p1_f32in", 4), ("ragged_b3_p2_f32in", 2)])
+def test_external_exchange_ranks_match_single(golden, case, world):
+    from convex_optimization_amd import distributed as D
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    B, IT = int(fx["BLOCK"]), int(fx["ITER_MAX"])
+    ranks = []
+    for g in range(world):
+        gc = make_cls("float")(D.shard_columns(A, B, g, world), B, device=0)
+        gc.set_ranks(g, world)
+        gc.solver_reset(fx["b"], float(fx["mu"]), record_len=IT, use_graph=False)
+        ranks.append(gc)
+    for _ in range(IT):
+        for gc in ranks:
+            gc.solver_phase(0)
+        torch.cuda.synchronize()
+        total = sum(gc.exchange_buffer().clone() for gc in ranks)
+        for gc in ranks:
+            gc.exchange_buffer().copy_(total)
+        torch.cuda.synchronize()
+        for gc in ranks:
+            gc.solver_phase(1)
+    x = D.assemble_x([gc.solver_x() for gc in ranks], B)
+    ref = fx["x"].reshape(-1)
+    assert rel(x, ref) <= 1e-9, rel(x, ref)
+    errs = [gc.solver_records()[0] for gc in ranks]
+    np.testing.assert_array_equal(errs[0], errs[1])
+    np.testing.assert_allclose(errs[0][:IT], fx["err_iter"][:IT], rtol=1e-6, atol=1e-9)
+
+
+def test_tuning_knobs_do_not_change_results(golden):
+    fx = golden("c1_b2_p4_f32in")
+    A = oracle.fixture_A(fx)
+    gc = make_cls("float")(A, 2, device=0)
+    base = gc.run(fx["b"], float(fx["mu"]), 50)["x"]
+    for key, val in [("nt_loads", 0), ("tail_permille", 0), ("reverse_rows", 1), ("tail_permille", 1000),
+                     ("nt_loads", 1)]:
+        gc.set_tuning(key, val)
+        np.testing.assert_array_equal(gc.run(fx["b"], float(fx["mu"]), 50)["x"], base)
