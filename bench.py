@@ -164,11 +164,12 @@ def cpu_baseline(gc, b, mu, seconds):
                       f"{H}x{gc.Block * W} fp32 A and b, {threads} OpenMP threads (fp64 arithmetic)"}
 
 
-def pmc_traffic(workload_key):
+def pmc_traffic(workload_key, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        data = json.load(open(path))
-        return data.get(workload_key)
+        return float(json.load(open(path))[workload_key][kernel]["hbm_bytes"])
     except Exception:
         return None
 
@@ -190,7 +191,7 @@ def main():
     dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(m, w, sa)
     achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
     workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}"
-    traffic = pmc_traffic(workload_key)
+    traffic = pmc_traffic(workload_key, "k_colpass" if dom == "colpass" else "k_rowpass")
     out = {
         "metric": METRIC,
         "value": iters_s_graph * G,
@@ -223,6 +224,8 @@ def main():
             "bound": "hbm", "kernel": "k_colpass<float,0> (A^T r)" if dom == "colpass" else "k_rowpass<float> (A D)",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+            if traffic else None,
             "alg_bytes_per_launch": dom_bytes,
             "avg_launch_ms": kms[dom],
         },
