@@ -164,6 +164,40 @@ def cpu_baseline(gc, b, mu, seconds):
                       f"{H}x{gc.Block * W} fp32 A and b, {threads} OpenMP threads (fp64 arithmetic)"}
 
 
+def vendor_yardstick(gc, reps=20):
+    """Speed yardstick only (the reference's cuBLAS classes):
+    PyTorch's ROCm GEMV (rocBLAS/hipBLASLt, fp32 accumulation) for the same two
+    passes, A^T r and A d, on the same resident fp32 A.  Not parity-equivalent
+    (fp32 accumulation); reported beside the solver, never as `value`."""
+    import torch
+    A = gc._A_dev
+    if A.dim() != 2 or A.dtype != torch.float32:
+        return None
+    H, K = A.shape
+    r = torch.randn(H, device=A.device)
+    d = torch.randn(K, device=A.device)
+    for _ in range(3):
+        torch.mv(A.t(), r)
+        torch.mv(A, d)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        torch.mv(A.t(), r)
+    e1.record()
+    torch.cuda.synchronize()
+    t_mtv = e0.elapsed_time(e1) / reps
+    e0.record()
+    for _ in range(reps):
+        torch.mv(A, d)
+    e1.record()
+    torch.cuda.synchronize()
+    t_mv = e0.elapsed_time(e1) / reps
+    return {"what": "torch.mv (rocBLAS/hipBLASLt) fp32 GEMV pair on the same A, fp32 accumulation",
+            "mtv_ms": t_mtv, "mv_ms": t_mv,
+            "mtv_GBps": H * K * 4 / t_mtv / 1e6, "mv_GBps": H * K * 4 / t_mv / 1e6}
+
+
 def pmc_traffic(workload_key, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
@@ -239,6 +273,8 @@ def main():
                          "config": f"m={m} n={args.n_per_gpu} split {G} ways ({strong['w_local']} cols/GPU)",
                          "kernel_avg_ms": strong["kernel_ms"]}
         res = strong
+    if G == 1 and args.type == "float":
+        out["config"]["vendor_gemv_yardstick"] = vendor_yardstick(res["gc"])
     if G == 1 and ctx.rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds)
     if ctx.rank == 0:

@@ -99,3 +99,24 @@ def test_hybrid_driver_semantics(golden, case):
     assert np.linalg.norm(drv.x.reshape(-1) - x) <= 1e-9 * np.linalg.norm(x)
     T = drv.iters
     np.testing.assert_allclose(err_iter[:T], fx["err_iter"][:T], rtol=1e-4, atol=1e-10)
+
+
+def test_results_files_roundtrip_and_figure(tmp_path):
+    from convex_optimization_amd import results
+    IT = 10
+    time_iter = np.linspace(0, 1, IT + 1)
+    err_iter = np.logspace(0, -5, IT)
+    results.save_performance("GPU", time_iter, err_iter, directory=str(tmp_path), iters=7)
+    results.save_performance("CPU", time_iter * 3, err_iter, directory=str(tmp_path))
+    data = results.load_performance(str(tmp_path))
+    np.testing.assert_array_equal(data["gpu_time"], time_iter[1:8])
+    np.testing.assert_array_equal(data["gpu_errors"], err_iter[:7])
+    assert data["cpu_time"].shape == (IT,)
+    png = results.compare_figure(str(tmp_path))
+    assert (tmp_path / "compare.png").exists() and png.endswith("compare.png")
+
+
+def test_list_aver_matches_reference_semantics():
+    from convex_optimization_amd.results import list_aver
+    assert list_aver([[1, 2, 3], [3, 4], [5]]) == [3.0, 3.0, 3.0]
+    assert list_aver([]) == []
