@@ -39,12 +39,15 @@ def alg_bytes_iter(m, w, sa=4, sv=8, k=1):
 
 
 def alg_bytes_colpass(m, w, sa=4):
-    """k_colpass per launch: read A_b (m x w), r (m fp64), write g-partials once (w fp64)."""
+    """A^T s11 pass per launch (k_iter_a / k_colpass): read A_b (m x w) and s11
+    (m fp64), produce g once (w fp64).  The shrink's x/D vector I/O is left out
+    (conservative)."""
     return m * w * sa + 8 * m + 8 * w
 
 
 def alg_bytes_rowpass(m, w, sa=4):
-    """k_rowpass per launch: read A_b (m x w), D (w fp64), write s23 once (m fp64)."""
+    """A D pass per launch (k_iter_b / k_rowpass): read A_b (m x w), D (w fp64),
+    produce s23 once (m fp64)."""
     return m * w * sa + 8 * w + 8 * m
 
 
@@ -61,6 +64,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=20190325)
+    ap.add_argument("--fused", type=int, default=0, help="1: two-launch fused iteration; 0 (default): five kernels")
     return ap.parse_args()
 
 
@@ -123,6 +127,7 @@ def timed_window(ctx, gc, steps, graph):
 
 def measure(ctx, args, m, n_total):
     gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed)
+    gc.set_tuning("fused", args.fused)
     # graph replay needs per-kernel events off; timing mode launches eagerly with
     # HIP events around every kernel on the solver stream.
     gc.solver_reset(b, mu, use_graph=True)
@@ -225,7 +230,9 @@ def main():
     dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(m, w, sa)
     achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
     workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}"
-    traffic = pmc_traffic(workload_key, "k_colpass" if dom == "colpass" else "k_rowpass")
+    kname = {("colpass", 1): "k_iter_a", ("rowpass", 1): "k_iter_b",
+             ("colpass", 0): "k_colpass", ("rowpass", 0): "k_rowpass"}[(dom, int(args.fused))]
+    traffic = pmc_traffic(workload_key, kname)
     out = {
         "metric": METRIC,
         "value": iters_s_graph * G,
@@ -250,12 +257,14 @@ def main():
             "alg_bytes_per_iter_per_gpu": alg_bytes_iter(m, w, sa),
             "hbm_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(m, w, sa),
             "iter_roofline_frac": iters_s_graph * alg_bytes_iter(m, w, sa) / (HBM_PEAK_GBS * 1e9),
-            "launch_mode": "hipGraph replay of one iteration (value); eager + HIP events (kernel times)",
+            "launch_mode": "hipGraph replay of one iteration (value); eager + HIP events (kernel times)", "fused": args.fused,
             "iters_per_s_eager_with_events": iters_s_ev,
             "kernel_avg_ms": kms,
         },
         "roofline": {
-            "bound": "hbm", "kernel": "k_colpass<float,0> (A^T r)" if dom == "colpass" else "k_rowpass<float> (A D)",
+            "bound": "hbm",
+            "kernel": kname + (" (A^T s11 pass + segment-finisher shrink)" if dom == "colpass"
+                               else " (A D pass + row-chunk finishers + line search)"),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"

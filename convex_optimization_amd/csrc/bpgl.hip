@@ -19,6 +19,7 @@
 
 #include "../../include/bpgl.h"
 #include "bpgl_kernels.h"
+#include "bpgl_fused.h"
 
 using namespace bpgl;
 
@@ -48,6 +49,7 @@ int fail(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr int kTimedKinds = 7;
+constexpr int kGraphIters = 8;
 constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
@@ -75,18 +77,26 @@ struct bpgl_ctx {
     bool external = false;   // nranks > 1 with the exchange done by the caller
     // solver
     bool solver = false, use_graph = false;
-    hipGraphExec_t gexec = nullptr;
+    hipGraphExec_t gexec = nullptr;     // one iteration
+    hipGraphExec_t gexec_k = nullptr;   // kGraphIters iterations (amortises the per-replay gap)
     // timing
     bool timing = false;
     std::vector<hipEvent_t> evs;   // (kinds + 1) events per timed iteration
     int64_t timed_iters = 0;
+    bool kind_used[kTimedKinds] = {};
     double wall_tick_s = 1e-8;
     int reverse_rows = 0;
+    int fused = 0;
     int nt_loads = 1;
     int tail_permille = 120;
 };
 
 namespace {
+
+void drop_graphs(bpgl_ctx* c) {
+    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    if (c->gexec_k) { hipGraphExecDestroy(c->gexec_k); c->gexec_k = nullptr; }
+}
 
 void geometry(bpgl_ctx* c) {
     const int V = vec_elems(c->dtype);
@@ -115,7 +125,7 @@ struct Carve {
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, total;
+    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -126,7 +136,9 @@ Layout layout(const bpgl_ctx* c) {
     L.g = k.take(8 * c->wp);
     L.D = k.take(8 * c->wp);
     L.parts = k.take(8 * 4 * (int64_t)c->nparts);
-    L.parts2 = k.take(8 * 2 * cdiv(c->m, kRowsPerReduce));
+    L.parts2 = k.take(8 * 2 * std::max<int64_t>(cdiv(c->m, kRowsPerReduce), c->nchunk));
+    L.Dbuf = k.take(8 * 2 * c->wp);
+    L.cnt = k.take(8 * ((int64_t)c->nseg + c->nchunk));
     L.comm = k.take(8 * (c->m + 2 + kMaxRanks));
     L.r = k.take(8 * c->m);
     L.Ax = k.take(8 * (int64_t)c->nblock * c->m);
@@ -173,6 +185,27 @@ int rowpass(bpgl_ctx* c, const double* d, double* slab, int fixed_block) {
     }
 }
 
+template <typename T>
+int launch_iter(bpgl_ctx* c, int which) {
+    if (which == 0) {
+        if (c->nt_loads) hipLaunchKernelGGL((k_iter_a<T, true>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
+        else hipLaunchKernelGGL((k_iter_a<T, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_iter_a");
+    } else {
+        if (c->nt_loads) hipLaunchKernelGGL((k_iter_b<T, true>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
+        else hipLaunchKernelGGL((k_iter_b<T, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_iter_b");
+    }
+    return 0;
+}
+int iter_kernel(bpgl_ctx* c, int which) {
+    switch (c->dtype) {
+        case BPGL_F32: return launch_iter<float>(c, which);
+        case BPGL_F64: return launch_iter<double>(c, which);
+        default: return launch_iter<bf16_t>(c, which);
+    }
+}
+
 int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) {
     hipLaunchKernelGGL(k_rowreduce, dim3((unsigned)cdiv(c->m, kRowsPerReduce)), dim3(kThreads), 0, c->stream,
                        c->p, slab, out, mode);
@@ -197,16 +230,57 @@ void ev_record(bpgl_ctx* c, int64_t it, int kind, int end) {
         c->evs.push_back(e);
     }
     hipEventRecord(c->evs[idx], c->stream);
+    c->kind_used[kind] = true;
 }
 
-// One block update, enqueued on c->stream.  The block index and every
-// iteration-dependent value are read on the device from the state words, so
-// the same launch sequence (or its captured graph) serves every iteration.
+// Fused iteration (tuning key "fused"): phase 0 = k_iter_a, k_iter_b [, all-reduce,
+// k_step_fused]; with caller-side exchange, phase 1 = k_step_fused.  The x / Ax
+// update of each iteration is applied by the next one (bpgl_fused.h).
+int enqueue_phase_fused(bpgl_ctx* c, int64_t it, int phase) {
+    int rc;
+    if (phase == 0) {
+        ev_record(c, it, 0, 0);
+        if ((rc = iter_kernel(c, 0))) return rc;
+        ev_record(c, it, 0, 1);
+        ev_record(c, it, 2, 0);
+        if ((rc = iter_kernel(c, 1))) return rc;
+        ev_record(c, it, 2, 1);
+        if (c->comm) {
+            ev_record(c, it, 4, 0);
+            ncclResult_t nr = ncclAllReduce(c->p.comm, c->p.comm, (size_t)(c->m + 2 + c->nranks), ncclFloat64,
+                                            ncclSum, c->comm, c->stream);
+            if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
+            ev_record(c, it, 4, 1);
+            ev_record(c, it, 5, 0);
+            hipLaunchKernelGGL(k_step_fused, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
+            LAUNCH_CHECK("k_step_fused");
+            ev_record(c, it, 5, 1);
+        }
+    } else if (c->external) {
+        hipLaunchKernelGGL(k_step_fused, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_step_fused");
+    }
+    return 0;
+}
+
+// apply the deferred update of the last fused iteration (no-op when none is pending)
+int finalize_fused(bpgl_ctx* c) {
+    if (!c->fused || !c->solver) return 0;
+    const int64_t n = std::max<int64_t>(c->wp, c->m);
+    const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(n, kThreads), 1024);
+    hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(kThreads), 0, c->stream, c->p);
+    LAUNCH_CHECK("k_finalize");
+    hipLaunchKernelGGL(k_clear_pending, dim3(1), dim3(64), 0, c->stream, c->p);
+    LAUNCH_CHECK("k_clear_pending");
+    return 0;
+}
+
 // phase 0: colpass, shrink, rowpass, rowreduce [, allreduce, step]; phase 1: update.
 // With the caller doing the exchange (external ranks) phase 0 stops after
 // rowreduce and phase 1 starts with the step.
 int enqueue_phase(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
+    if (c->fused) return enqueue_phase_fused(c, it, phase);
     const bool multi = c->comm != nullptr || c->external;
     if (phase == 0) {
         ev_record(c, it, 0, 0);
@@ -305,7 +379,7 @@ int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_lo
 void bpgl_destroy(bpgl_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
-    if (c->gexec) hipGraphExecDestroy(c->gexec);
+    drop_graphs(c);
     for (auto e : c->evs) hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->own_stream) hipStreamDestroy(c->stream);
@@ -367,6 +441,9 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     p.D = (double*)(s + L.D);
     p.parts = (double*)(s + L.parts);
     p.parts2 = (double*)(s + L.parts2);
+    p.Dbuf = (double*)(s + L.Dbuf);
+    p.cnt_seg = (unsigned long long*)(s + L.cnt);
+    p.cnt_chunk = p.cnt_seg + c->nseg;
     p.reverse_rows = c->reverse_rows;
     p.tail_permille = c->tail_permille;
     p.comm = (double*)(s + L.comm);
@@ -379,10 +456,14 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s + L.st, 0, sizeof(DevState), c->stream));
     HIP_TRY(hipMemsetAsync(s + L.D, 0, 8 * c->wp, c->stream));
+    HIP_TRY(hipMemsetAsync(s + L.Dbuf, 0, 16 * c->wp, c->stream));
+    HIP_TRY(hipMemsetAsync(s + L.cnt, 0, 8 * ((int64_t)c->nseg + c->nchunk), c->stream));
+    if (8ll * c->nchunk * c->wp >= (1ll << 31) || 8ll * c->nseg * c->m >= (1ll << 31))
+        return fail(BPGL_E_ARG, "split-K slabs exceed 2 GiB (raise BPGL_TARGET_BLOCKS granularity)");
     c->bound = true;
     c->have_diag = false;
     c->solver = false;
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    drop_graphs(c);
     return 0;
 }
 
@@ -455,7 +536,7 @@ int bpgl_comm_init(bpgl_ctx* c, const void* uid, int rank, int nranks) {
     }
     c->p.has_comm = c->comm != nullptr;
     c->external = false;
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    drop_graphs(c);
     return 0;
 }
 
@@ -470,7 +551,7 @@ int bpgl_set_ranks(bpgl_ctx* c, int rank, int nranks) {
     c->p.nranks = nranks;
     c->p.has_comm = 0;
     c->external = nranks > 1;
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    drop_graphs(c);
     c->solver = false;
     return 0;
 }
@@ -481,7 +562,9 @@ int bpgl_solver_phase(bpgl_ctx* c, int phase) {
     if (!c->solver) return fail(BPGL_E_STATE, "bpgl_solver_reset has not been called");
     if (phase != 0 && phase != 1) return fail(BPGL_E_ARG, "phase must be 0 or 1");
     HIP_TRY(hipSetDevice(c->device));
-    return enqueue_phase(c, 0, phase);
+    if ((rc = enqueue_phase(c, 0, phase))) return rc;
+    if (phase == 1) return finalize_fused(c);
+    return 0;
 }
 
 double* bpgl_solver_exchange_buffer(bpgl_ctx* c, int64_t* count) {
@@ -524,21 +607,25 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
     hipLaunchKernelGGL(k_reset, dim3((unsigned)std::min<int64_t>(cdiv(c->m, kThreads), 1024)), dim3(kThreads), 0,
                        c->stream, p);
     LAUNCH_CHECK("k_reset");
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    drop_graphs(c);
     c->use_graph = use_graph != 0 && !c->external;
     if (c->use_graph) {
-        hipGraph_t graph = nullptr;
         const bool was_timing = c->timing;
         c->timing = false;
-        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        rc = enqueue_iteration(c, 0);
-        hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+        for (int variant = 0; variant < 2; ++variant) {
+            const int iters = variant == 0 ? 1 : kGraphIters;
+            hipGraph_t graph = nullptr;
+            HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            rc = 0;
+            for (int k = 0; k < iters && !rc; ++k) rc = enqueue_iteration(c, 0);
+            hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+            if (rc) { if (graph) hipGraphDestroy(graph); c->timing = was_timing; return rc; }
+            if (ec != hipSuccess) { c->timing = was_timing; return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec)); }
+            hipError_t ei = hipGraphInstantiate(variant == 0 ? &c->gexec : &c->gexec_k, graph, nullptr, nullptr, 0);
+            hipGraphDestroy(graph);
+            if (ei != hipSuccess) { c->timing = was_timing; return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei)); }
+        }
         c->timing = was_timing;
-        if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
-        if (ec != hipSuccess) return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
-        hipError_t ei = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
-        if (ei != hipSuccess) return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
     }
     c->solver = true;
     c->timed_iters = 0;
@@ -552,7 +639,10 @@ int bpgl_solver_step(bpgl_ctx* c, int64_t n_iter) {
     if (n_iter < 0) return fail(BPGL_E_ARG, "n_iter < 0");
     if (c->external) return fail(BPGL_E_STATE, "external-exchange ranks advance with bpgl_solver_phase");
     HIP_TRY(hipSetDevice(c->device));
-    for (int64_t i = 0; i < n_iter; ++i) {
+    int64_t i = 0;
+    if (!c->timing && c->gexec_k)
+        for (; i + kGraphIters <= n_iter; i += kGraphIters) HIP_TRY(hipGraphLaunch(c->gexec_k, c->stream));
+    for (; i < n_iter; ++i) {
         if (c->timing || !c->gexec) {
             if ((rc = enqueue_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
             if (c->timing) c->timed_iters++;
@@ -560,7 +650,7 @@ int bpgl_solver_step(bpgl_ctx* c, int64_t n_iter) {
             HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
         }
     }
-    return 0;
+    return finalize_fused(c);
 }
 
 int bpgl_solver_status(bpgl_ctx* c, int64_t* iters_done, int* stopped, int64_t* t_last, double* gamma,
@@ -597,7 +687,7 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "reverse_rows")) {
         c->reverse_rows = value != 0;
         c->p.reverse_rows = c->reverse_rows;
-        if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+        drop_graphs(c);
         c->solver = false;   // a new bpgl_solver_reset re-captures the iteration
         return 0;
     }
@@ -605,13 +695,19 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         if (value < 0 || value > 1000) return fail(BPGL_E_ARG, "tail_permille must be in [0, 1000]");
         c->tail_permille = (int)value;
         c->p.tail_permille = c->tail_permille;
-        if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "fused")) {
+        c->fused = value != 0;
+        drop_graphs(c);
         c->solver = false;
         return 0;
     }
     if (!strcmp(key, "nt_loads")) {
         c->nt_loads = value != 0;
-        if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+        drop_graphs(c);
         c->solver = false;
         return 0;
     }
@@ -622,6 +718,7 @@ int bpgl_set_kernel_timing(bpgl_ctx* c, int enable) {
     if (!c) return fail(BPGL_E_ARG, "null context");
     c->timing = enable != 0;
     c->timed_iters = 0;
+    for (int k = 0; k < kTimedKinds; ++k) c->kind_used[k] = false;
     return 0;
 }
 
@@ -633,8 +730,7 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     const bool multi = c->comm != nullptr || c->external;
     for (int64_t it = 0; it < c->timed_iters; ++it) {
         for (int k = 0; k < kTimedKinds; ++k) {
-            if (!multi && (k == 4 || k == 5)) continue;
-            if (!c->comm && k == 4) continue;
+            if (!c->kind_used[k]) continue;
             float ms = 0.f;
             const size_t i0 = 2 * ((size_t)it * kTimedKinds + k);
             if (i0 + 1 >= c->evs.size()) continue;
@@ -645,6 +741,7 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     for (int k = 0; k < kTimedKinds; ++k) avg_ms[k] = c->timed_iters ? sum[k] / c->timed_iters : 0.0;
     if (samples) *samples = c->timed_iters;
     c->timed_iters = 0;
+    for (int k = 0; k < kTimedKinds; ++k) c->kind_used[k] = false;
     return 0;
 }
 

@@ -38,7 +38,9 @@ struct DevState {
     double r1, r2;        // line-search numerators (diagnostics)
     long long iters;      // iterations completed (update applied or stop reached)
     unsigned long long cnt_rowreduce;   // monotonic arrival counter of k_rowreduce blocks
-    long long pad[4];
+    long long pending;    // fused mode: the update of iteration t-1 is not yet applied to x / Ax
+    unsigned long long cnt_all;         // fused mode: arrivals of row-chunk finishers in k_iter_b
+    long long pad[2];
 };
 
 struct Params {
@@ -70,6 +72,10 @@ struct Params {
     DevState* st;
     double mu, err_bound;
     double wall_tick_s;   // seconds per wall_clock64() tick
+    // fused two-launch iteration (k_iter_a / k_iter_b)
+    double* Dbuf;                    // [2][wp]  direction of iterations with parity 0 / 1
+    unsigned long long* cnt_seg;     // [nseg]   arrivals per column segment (k_iter_a)
+    unsigned long long* cnt_chunk;   // [nchunk] arrivals per row chunk (k_iter_b)
 };
 
 // ---------------------------------------------------------------------------
@@ -277,6 +283,14 @@ __global__ __launch_bounds__(kThreads) void k_shrink(Params p) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long j = (long long)blockIdx.x * kColsPerShrink + lane;
     const long long jj = j < p.wp ? j : p.wp - 1;
+    // wave 0 issues its epilogue operands (diag, 1/diag, x) with the slab loads
+    double d_e = 0.0, rec_e = 0.0, x_e = 0.0;
+    if (wave == 0) {
+        const long long kx = (long long)mb * p.wp + jj;
+        d_e = p.diag[kx];
+        rec_e = p.rec[kx];
+        x_e = p.x[kx];
+    }
     double acc = 0.0;
     {
         int c = wave;
@@ -300,10 +314,9 @@ __global__ __launch_bounds__(kThreads) void k_shrink(Params p) {
         p.g[j] = g;
         double Dj = 0.0;
         if (j < p.w) {
-            const long long k = (long long)mb * p.wp + j;
-            const double d = p.diag[k], xj = p.x[k];
+            const double d = d_e, xj = x_e;
             const double rx = d * xj - g;                     // lasso.py:114
-            const double bx = p.rec[k] * soft_thr(rx, p.mu);  // lasso.py:115-117
+            const double bx = rec_e * soft_thr(rx, p.mu);     // lasso.py:115-117
             Dj = bx - xj;                                     // lasso.py:119
             abx = fabs(bx);
             ax = fabs(xj);
@@ -456,10 +469,10 @@ __device__ void finish_step(const Params& p, double rs, double ss, double l1bx, 
 }
 
 // fold the shrink partials (fixed order) : sum |Bx|, sum |x|, max err
-__device__ void fold_parts(const Params& p, double& a, double& b, double& e) {
+__device__ void fold_parts(const Params& p, int count, double& a, double& b, double& e) {
     __shared__ double sred[3][kWaves];
     a = 0.0; b = 0.0; e = 0.0;
-    for (int k = threadIdx.x; k < p.nparts; k += kThreads) {
+    for (int k = threadIdx.x; k < count; k += kThreads) {
         a += p.parts[4ll * k];
         b += p.parts[4ll * k + 1];
         const double ek = p.parts[4ll * k + 2];
@@ -503,18 +516,20 @@ __global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long i = (long long)blockIdx.x * kRowsPerReduce + lane;
     const long long ii = i < p.m ? i : p.m - 1;
+    // wave q sums segments q, q+4, q+8, ...: all of a batch of kBatch loads are
+    // issued before the (fixed-order) adds, so a wave pays one latency per batch
+    constexpr int kBatch = 16;
     double acc = 0.0;
-    {
-        int q = wave;
-#pragma unroll 4
-        for (; q + 3 * kWaves < p.nseg; q += 4 * kWaves) {
-            const double a0 = slab[(long long)q * p.m + ii];
-            const double a1 = slab[(long long)(q + kWaves) * p.m + ii];
-            const double a2 = slab[(long long)(q + 2 * kWaves) * p.m + ii];
-            const double a3 = slab[(long long)(q + 3 * kWaves) * p.m + ii];
-            acc = (((acc + a0) + a1) + a2) + a3;
+    for (int q0 = wave; q0 < p.nseg; q0 += kBatch * kWaves) {
+        double v[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int q = q0 + k * kWaves;
+            const int qq = q < p.nseg ? q : wave;
+            v[k] = slab[(long long)qq * p.m + ii];
         }
-        for (; q < p.nseg; q += kWaves) acc += slab[(long long)q * p.m + ii];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) acc += (q0 + k * kWaves < p.nseg) ? v[k] : 0.0;
     }
     __shared__ double red[kWaves][64];
     __shared__ int am_last;
@@ -528,7 +543,7 @@ __global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* 
     if (mode == 2) {
         if (blockIdx.x == 0) {
             double a, b, e;
-            fold_parts(p, a, b, e);
+            fold_parts(p, p.nparts, a, b, e);
             if (threadIdx.x == 0) {
                 out[p.m] = a;
                 out[p.m + 1] = b;
@@ -570,7 +585,7 @@ __global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* 
         ss = ((sq[0] + sq[1]) + sq[2]) + sq[3];
     }
     double a, b, e;
-    fold_parts(p, a, b, e);
+    fold_parts(p, p.nparts, a, b, e);
     if (threadIdx.x == 0) finish_step(p, rs, ss, a, b, e);
 }
 
@@ -643,7 +658,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(Params p) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         DevState* st = p.st;
-        st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0;
+        st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0; st->pending = 0;
         st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0;
         st->t_base = (long long)wall_clock64();
         if (p.time_iter) p.time_iter[0] = 0.0;

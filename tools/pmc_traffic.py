@@ -30,7 +30,11 @@ def per_launch(dirname, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row.get("Kernel_Name", "")
-                if "k_colpass" in name and ("Li0E" in name or ", 0," in name or "<float, 0" in name):
+                if "k_iter_a" in name:
+                    key = "k_iter_a"
+                elif "k_iter_b" in name:
+                    key = "k_iter_b"
+                elif "k_colpass" in name and ("Li0E" in name or ", 0," in name or "<float, 0" in name):
                     key = "k_colpass"
                 elif "k_rowpass" in name:
                     key = "k_rowpass"

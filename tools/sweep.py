@@ -20,9 +20,10 @@ def main():
     ap.add_argument("--block", type=int, default=1)
     ap.add_argument("--type", default="float")
     ap.add_argument("--targets", default="2048")
-    ap.add_argument("--reverse", default="1")
+    ap.add_argument("--reverse", default="0")
     ap.add_argument("--nt", default="1")
-    ap.add_argument("--tails", default="0")
+    ap.add_argument("--tails", default="120")
+    ap.add_argument("--fused", default="0")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
@@ -34,8 +35,9 @@ def main():
         os.environ["BPGL_TARGET_BLOCKS"] = str(tb)
         gc, b, mu, _ = device_instance(a.m, a.n, 0.4, a.block, TYPE=a.type, seed=1, device=0)
         geo = gc.geometry()
-        for rev, nt, tail in [(int(r), int(n), int(t)) for r in a.reverse.split(",") for n in a.nt.split(",")
-                              for t in a.tails.split(",")]:
+        for rev, nt, tail, fu in [(int(r), int(n), int(t), int(f)) for r in a.reverse.split(",")
+                                  for n in a.nt.split(",") for t in a.tails.split(",") for f in a.fused.split(",")]:
+            gc.set_tuning("fused", fu)
             gc.set_tuning("reverse_rows", rev)
             gc.set_tuning("nt_loads", nt)
             gc.set_tuning("tail_permille", tail)
@@ -54,7 +56,7 @@ def main():
             gc.solver_step(a.steps // 2)
             kt, _ = gc.kernel_times()
             gc.set_kernel_timing(False)
-            rec = dict(target=tb, reverse=rev, nt=nt, tail=tail, geometry=geo, iters_per_s=best,
+            rec = dict(target=tb, reverse=rev, nt=nt, tail=tail, fused=fu, geometry=geo, iters_per_s=best,
                        kernel_us={k: round(v * 1e3, 2) for k, v in kt.items()})
             print(json.dumps(rec), flush=True)
             out.append(rec)
