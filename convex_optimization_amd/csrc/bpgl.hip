@@ -87,6 +87,7 @@ struct bpgl_ctx {
     double wall_tick_s = 1e-8;
     int reverse_rows = 0;
     int fused = 0;
+    int col_mode = 1;      // k_colpass row schedule (see launch_colpass)
     int nt_loads = 1;
     int tail_permille = 120;
 };
@@ -150,16 +151,28 @@ Layout layout(const bpgl_ctx* c) {
 
 dim3 grid_tiles(const bpgl_ctx* c) { return dim3((unsigned)((int64_t)c->nseg * c->nchunk)); }
 
-template <typename T>
-int launch_colpass(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_block) {
+template <typename T, int RPT, bool PIPE>
+int launch_colpass_r(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_block) {
     if (mode == 0 && c->nt_loads)
-        hipLaunchKernelGGL((k_colpass<T, 0, true>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+        hipLaunchKernelGGL((k_colpass<T, 0, true, RPT, PIPE>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec,
+                           slab, fixed_block);
     else if (mode == 0)
-        hipLaunchKernelGGL((k_colpass<T, 0, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+        hipLaunchKernelGGL((k_colpass<T, 0, false, RPT, PIPE>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec,
+                           slab, fixed_block);
     else
-        hipLaunchKernelGGL((k_colpass<T, 1, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec, slab, fixed_block);
+        hipLaunchKernelGGL((k_colpass<T, 1, false, 2, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p, vec,
+                           slab, fixed_block);
     LAUNCH_CHECK("k_colpass");
     return 0;
+}
+// col_mode: 0 = 2 rows per trip, 1 = 4 rows per trip, 2 = 2 rows per trip software-pipelined
+template <typename T>
+int launch_colpass(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_block) {
+    switch (c->col_mode) {
+        case 1: return launch_colpass_r<T, 4, false>(c, mode, vec, slab, fixed_block);
+        case 2: return launch_colpass_r<T, 2, true>(c, mode, vec, slab, fixed_block);
+        default: return launch_colpass_r<T, 2, false>(c, mode, vec, slab, fixed_block);
+    }
 }
 int colpass(bpgl_ctx* c, int mode, const double* vec, double* slab, int fixed_block) {
     switch (c->dtype) {
@@ -695,6 +708,13 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         if (value < 0 || value > 1000) return fail(BPGL_E_ARG, "tail_permille must be in [0, 1000]");
         c->tail_permille = (int)value;
         c->p.tail_permille = c->tail_permille;
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "col_mode")) {
+        if (value < 0 || value > 2) return fail(BPGL_E_ARG, "col_mode must be 0, 1 or 2");
+        c->col_mode = (int)value;
         drop_graphs(c);
         c->solver = false;
         return 0;

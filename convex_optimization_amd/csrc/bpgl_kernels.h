@@ -146,46 +146,79 @@ __device__ __forceinline__ double wave_max(double v) {
 // R rows; the 4 waves split the rows (wave q: rows q, q+4, ...) and sum their
 // fp64 partials through LDS in a fixed order.
 // ---------------------------------------------------------------------------
-// rows [i, istop) of one wave (step 2 x 4 rows: rows i and i + 4 per trip)
-template <typename T, int MODE, bool NT>
-__device__ __forceinline__ void colpass_span(const T* __restrict__ Ab, long long lda, const long long (&col)[kU],
-                                             const double* __restrict__ vec, long long& i, long long istop,
-                                             long long i1, double (&acc)[kU][VecT<T>::N]) {
+// One "trip" of a wave in k_colpass: RPT rows (i, i+4, ..., i+4(RPT-1)), kU
+// sixteen-byte loads per row.  Rows at or past i1 are clamped to row i (in
+// bounds) and get a zero weight.
+template <typename T, int MODE, bool NT, int RPT>
+__device__ __forceinline__ void colpass_load(const T* __restrict__ Ab, long long lda, const long long (&col)[kU],
+                                             const double* __restrict__ vec, long long i, long long i1,
+                                             typename VecT<T>::raw (&a)[RPT][kU], double (&sc)[RPT]) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        long long r = i + k * kWaves;
+        const bool ok = r < i1;
+        r = ok ? r : i;
+        sc[k] = (MODE == 0) ? vec[r] : 1.0;
+        sc[k] = ok ? sc[k] : 0.0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) a[k][u] = ldv<T, NT>(Ab + r * lda + col[u]);
+    }
+}
+template <typename T, int MODE, int RPT>
+__device__ __forceinline__ void colpass_fma(const typename VecT<T>::raw (&a)[RPT][kU], const double (&sc)[RPT],
+                                            double (&acc)[kU][VecT<T>::N]) {
     constexpr int V = VecT<T>::N;
-    using raw = typename VecT<T>::raw;
-    for (; i < istop; i += 2 * kWaves) {
-        const bool two = i + kWaves < i1;
-        const long long i2 = two ? i + kWaves : i;
-        const T* r0 = Ab + i * lda;
-        const T* r1 = Ab + i2 * lda;
-        raw a0[kU], a1[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) a0[u] = ldv<T, NT>(r0 + col[u]);
+    for (int u = 0; u < kU; ++u) {
 #pragma unroll
-        for (int u = 0; u < kU; ++u) a1[u] = ldv<T, NT>(r1 + col[u]);
-        double s0 = 1.0, s1 = 1.0;
-        if (MODE == 0) { s0 = vec[i]; s1 = vec[i2]; }   // i2 == i when !two: in bounds
-        s1 = two ? s1 : 0.0;
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            double v0[V], v1[V];
-            VecT<T>::cvt(a0[u], v0);
-            VecT<T>::cvt(a1[u], v1);
+        for (int k = 0; k < RPT; ++k) {
+            double v[V];
+            VecT<T>::cvt(a[k][u], v);
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                if (MODE == 0) {
-                    acc[u][e] = fma(v0[e], s0, acc[u][e]);
-                    acc[u][e] = fma(v1[e], s1, acc[u][e]);
-                } else {
-                    acc[u][e] = fma(v0[e], v0[e], acc[u][e]);
-                    acc[u][e] = fma(v1[e] * s1, v1[e], acc[u][e]);
-                }
+                if (MODE == 0) acc[u][e] = fma(v[e], sc[k], acc[u][e]);
+                else acc[u][e] = fma(v[e] * sc[k], v[e], acc[u][e]);
             }
         }
     }
 }
 
-template <typename T, int MODE, bool NT>
+// rows [i, istop) of one wave, RPT rows per trip.  PIPE: the next trip's loads
+// are issued before the current trip's FMAs (2 x RPT x kU loads in flight per
+// lane, at a higher register cost).  Every accumulator sees its rows in
+// increasing order, so results depend on neither RPT nor PIPE.
+template <typename T, int MODE, bool NT, int RPT, bool PIPE>
+__device__ __forceinline__ void colpass_span(const T* __restrict__ Ab, long long lda, const long long (&col)[kU],
+                                             const double* __restrict__ vec, long long& i, long long istop,
+                                             long long i1, double (&acc)[kU][VecT<T>::N]) {
+    using raw = typename VecT<T>::raw;
+    constexpr long long step = (long long)RPT * kWaves;
+    if (i >= istop) return;
+    if constexpr (!PIPE) {
+        for (; i < istop; i += step) {
+            raw a[RPT][kU];
+            double sa[RPT];
+            colpass_load<T, MODE, NT, RPT>(Ab, lda, col, vec, i, i1, a, sa);
+            colpass_fma<T, MODE, RPT>(a, sa, acc);
+        }
+    } else {
+        raw a[RPT][kU], b[RPT][kU];
+        double sa[RPT], sb[RPT];
+        colpass_load<T, MODE, NT, RPT>(Ab, lda, col, vec, i, i1, a, sa);
+        for (;;) {
+            if (i + step >= istop) { colpass_fma<T, MODE, RPT>(a, sa, acc); i += step; return; }
+            colpass_load<T, MODE, NT, RPT>(Ab, lda, col, vec, i + step, i1, b, sb);
+            colpass_fma<T, MODE, RPT>(a, sa, acc);
+            i += step;
+            if (i + step >= istop) { colpass_fma<T, MODE, RPT>(b, sb, acc); i += step; return; }
+            colpass_load<T, MODE, NT, RPT>(Ab, lda, col, vec, i + step, i1, a, sa);
+            colpass_fma<T, MODE, RPT>(b, sb, acc);
+            i += step;
+        }
+    }
+}
+
+template <typename T, int MODE, bool NT, int RPT, bool PIPE>
 __global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __restrict__ vec,
                                                       double* __restrict__ slab, int fixed_block) {
     constexpr int V = VecT<T>::N;
@@ -221,9 +254,9 @@ __global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __
     long long i = i0 + wave;
     if (NT) {
         const long long isplit = i1 - ((i1 - i0) * p.tail_permille) / 1000;
-        colpass_span<T, MODE, true>(Ab, p.lda, col, vec, i, isplit, i1, acc);
+        colpass_span<T, MODE, true, RPT, PIPE>(Ab, p.lda, col, vec, i, isplit, i1, acc);
     }
-    colpass_span<T, MODE, false>(Ab, p.lda, col, vec, i, i1, i1, acc);
+    colpass_span<T, MODE, false, RPT, PIPE>(Ab, p.lda, col, vec, i, i1, i1, acc);
     // cross-wave reduction in a fixed order (wave 0 + 1 + 2 + 3)
     __shared__ double red[kWaves][kU * V][64];
 #pragma unroll

@@ -269,7 +269,7 @@ def test_tuning_knobs_do_not_change_results(golden, fused):
     gc.set_tuning("fused", fused)
     base = gc.run(fx["b"], float(fx["mu"]), 50)["x"]
     for key, val in [("nt_loads", 0), ("tail_permille", 0), ("reverse_rows", 1), ("tail_permille", 1000),
-                     ("nt_loads", 1)]:
+                     ("nt_loads", 1), ("col_mode", 1), ("col_mode", 2), ("col_mode", 0)]:
         gc.set_tuning(key, val)
         np.testing.assert_array_equal(gc.run(fx["b"], float(fx["mu"]), 50)["x"], base)
 
