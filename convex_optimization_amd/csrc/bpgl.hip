@@ -137,7 +137,7 @@ Layout layout(const bpgl_ctx* c) {
     L.g = k.take(8 * c->wp);
     L.D = k.take(8 * c->wp);
     L.parts = k.take(8 * 4 * (int64_t)c->nparts);
-    L.parts2 = k.take(8 * 2 * std::max<int64_t>(cdiv(c->m, kRowsPerReduce), c->nchunk));
+    L.parts2 = k.take(8 * 2 * std::max<int64_t>(kMaxReduceBlocks, c->nchunk));
     L.Dbuf = k.take(8 * 2 * c->wp);
     L.cnt = k.take(8 * ((int64_t)c->nseg + c->nchunk));
     L.comm = k.take(8 * (c->m + 2 + kMaxRanks));
@@ -219,10 +219,20 @@ int iter_kernel(bpgl_ctx* c, int which) {
     }
 }
 
+unsigned rowreduce_blocks(const bpgl_ctx* c) {
+    return (unsigned)std::min<int64_t>(cdiv(c->m, kRowsPerReduce), kMaxReduceBlocks);
+}
 int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) {
-    hipLaunchKernelGGL(k_rowreduce, dim3((unsigned)cdiv(c->m, kRowsPerReduce)), dim3(kThreads), 0, c->stream,
-                       c->p, slab, out, mode);
+    const dim3 g(rowreduce_blocks(c)), b(kThreads);
+    // one batch of loads per wave covers the segments: 4 waves x BATCH >= nseg
+    if (c->nseg <= 4) hipLaunchKernelGGL(k_rowreduce<1>, g, b, 0, c->stream, c->p, slab, out, mode);
+    else if (c->nseg <= 16) hipLaunchKernelGGL(k_rowreduce<4>, g, b, 0, c->stream, c->p, slab, out, mode);
+    else hipLaunchKernelGGL(k_rowreduce<16>, g, b, 0, c->stream, c->p, slab, out, mode);
     LAUNCH_CHECK("k_rowreduce");
+    if (mode == 1) {
+        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, c->p, (int)rowreduce_blocks(c));
+        LAUNCH_CHECK("k_linesearch");
+    }
     return 0;
 }
 

@@ -37,47 +37,6 @@
 
 namespace bpgl {
 
-// write-through (sc1) accesses.  8-byte scalars: agent-scope relaxed atomics;
-// split-K slabs: buffer loads / stores with the sc1 cache-policy bit (aux 16),
-// which the compiler batches like ordinary loads.
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-constexpr int kSC1 = 16;
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double* base, long long bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ void bst2_sc1(__amdgpu_buffer_rsrc_t r, long long off, double a, double b) {
-    const double v[2] = {a, b};
-    u32x4 u;
-    __builtin_memcpy(&u, v, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)off, 0, kSC1);
-}
-__device__ __forceinline__ void bst1_sc1(__amdgpu_buffer_rsrc_t r, long long off, double a) {
-    u32x2 u;
-    __builtin_memcpy(&u, &a, 8);
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)off, 0, kSC1);
-}
-__device__ __forceinline__ void bld2_sc1(__amdgpu_buffer_rsrc_t r, long long off, double& a, double& b) {
-    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSC1);
-    double v[2];
-    __builtin_memcpy(v, &u, 16);
-    a = v[0];
-    b = v[1];
-}
-__device__ __forceinline__ double bld1_sc1(__amdgpu_buffer_rsrc_t r, long long off) {
-    const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kSC1);
-    double v;
-    __builtin_memcpy(&v, &u, 8);
-    return v;
-}
-
 // every storing wave drains, block barrier, one lane arrives; true in every
 // thread of the block that completed the count.
 __device__ __forceinline__ bool arrive_last(unsigned long long* cnt, unsigned long long expected) {

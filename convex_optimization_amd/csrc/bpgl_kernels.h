@@ -37,7 +37,7 @@ struct DevState {
     double err;           // error criterion of the last iteration
     double r1, r2;        // line-search numerators (diagnostics)
     long long iters;      // iterations completed (update applied or stop reached)
-    unsigned long long cnt_rowreduce;   // monotonic arrival counter of k_rowreduce blocks
+    unsigned long long reserved0;
     long long pending;    // fused mode: the update of iteration t-1 is not yet applied to x / Ax
     unsigned long long cnt_all;         // fused mode: arrivals of row-chunk finishers in k_iter_b
     long long pad[2];
@@ -501,6 +501,47 @@ __device__ void finish_step(const Params& p, double rs, double ss, double l1bx, 
     st->t = t + 1;
 }
 
+// write-through (sc1) accesses.  8-byte scalars: agent-scope relaxed atomics;
+// split-K slabs: buffer loads / stores with the sc1 cache-policy bit (aux 16),
+// which the compiler batches like ordinary loads.
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+constexpr int kSC1 = 16;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double* base, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void bst2_sc1(__amdgpu_buffer_rsrc_t r, long long off, double a, double b) {
+    const double v[2] = {a, b};
+    u32x4 u;
+    __builtin_memcpy(&u, v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)off, 0, kSC1);
+}
+__device__ __forceinline__ void bst1_sc1(__amdgpu_buffer_rsrc_t r, long long off, double a) {
+    u32x2 u;
+    __builtin_memcpy(&u, &a, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)off, 0, kSC1);
+}
+__device__ __forceinline__ void bld2_sc1(__amdgpu_buffer_rsrc_t r, long long off, double& a, double& b) {
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSC1);
+    double v[2];
+    __builtin_memcpy(v, &u, 16);
+    a = v[0];
+    b = v[1];
+}
+__device__ __forceinline__ double bld1_sc1(__amdgpu_buffer_rsrc_t r, long long off) {
+    const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kSC1);
+    double v;
+    __builtin_memcpy(&v, &u, 8);
+    return v;
+}
+
 // fold the shrink partials (fixed order) : sum |Bx|, sum |x|, max err
 __device__ void fold_parts(const Params& p, int count, double& a, double& b, double& e) {
     __shared__ double sred[3][kWaves];
@@ -523,100 +564,91 @@ __device__ void fold_parts(const Params& p, int count, double& a, double& b, dou
     for (int q = 1; q < kWaves; ++q) e = (sred[2][q] > e || sred[2][q] != sred[2][q]) ? sred[2][q] : e;
 }
 
-__device__ __forceinline__ void st_agent(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_agent(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
 // ---------------------------------------------------------------------------
-// rowreduce: out[i] = sum_{q < nseg} slab_s[q][i]  (block = 64 rows x 4 waves,
-// wave q sums segments q, q+4, ...; fixed-order combine).
+// rowreduce: out[i] = sum_{q < nseg} slab_s[q][i].  Block = 64 rows x 4 waves,
+// wave w sums segments w, w+4, ... in batches of BATCH loads issued before the
+// fixed-order adds; grid-stride over 64-row groups.
 //   mode 0 : plain reduction (bpgl_mv API)
-//   mode 1 : solver, single rank: per-block partials of r.s23 and s23.s23, and
-//            the LAST arriving block (agent-scope counter, write-through
-//            partials) folds all partials and runs the line search.
-//   mode 2 : solver, multi rank: out = this rank's partial s23; block 0 adds
-//            [sum |Bx|, sum |x|, err slot] for the all-reduce; k_step follows.
+//   mode 1 : solver, one rank: also this block's share of r.s23 and s23.s23
+//            into parts2[block] (k_linesearch folds them)
+//   mode 2 : solver, several ranks: out = this rank's share of s23; block 0
+//            adds [sum |Bx|, sum |x|, err slot] for the all-reduce (k_step)
 // ---------------------------------------------------------------------------
 constexpr int kRowsPerReduce = 64;
+constexpr int kMaxReduceBlocks = 2048;
+template <int BATCH>
 __global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* __restrict__ slab,
                                                         double* __restrict__ out, int mode) {
     if (mode && p.st->done) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const long long i = (long long)blockIdx.x * kRowsPerReduce + lane;
-    const long long ii = i < p.m ? i : p.m - 1;
-    // wave q sums segments q, q+4, q+8, ...: all of a batch of kBatch loads are
-    // issued before the (fixed-order) adds, so a wave pays one latency per batch
-    constexpr int kBatch = 16;
-    double acc = 0.0;
-    for (int q0 = wave; q0 < p.nseg; q0 += kBatch * kWaves) {
-        double v[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            const int q = q0 + k * kWaves;
-            const int qq = q < p.nseg ? q : wave;
-            v[k] = slab[(long long)qq * p.m + ii];
-        }
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) acc += (q0 + k * kWaves < p.nseg) ? v[k] : 0.0;
-    }
     __shared__ double red[kWaves][64];
-    __shared__ int am_last;
-    red[wave][lane] = acc;
-    __syncthreads();
-    double s = 0.0;
-    if (wave == 0 && i < p.m) {
-        s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-        out[i] = s;
-    }
-    if (mode == 2) {
-        if (blockIdx.x == 0) {
-            double a, b, e;
-            fold_parts(p, p.nparts, a, b, e);
-            if (threadIdx.x == 0) {
-                out[p.m] = a;
-                out[p.m + 1] = b;
-                for (int r = 0; r < p.nranks; ++r) out[p.m + 2 + r] = (r == p.rank) ? e : 0.0;
+    const long long ngroups = (p.m + kRowsPerReduce - 1) / kRowsPerReduce;
+    double rs = 0.0, ss = 0.0;
+    for (long long grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        const long long i = grp * kRowsPerReduce + lane;
+        const long long ii = i < p.m ? i : p.m - 1;
+        double acc = 0.0;
+        for (int q0 = wave; q0 < p.nseg; q0 += BATCH * kWaves) {
+            double v[BATCH];
+#pragma unroll
+            for (int k = 0; k < BATCH; ++k) {
+                const int q = q0 + k * kWaves;
+                v[k] = slab[(long long)(q < p.nseg ? q : q0) * p.m + ii];
+            }
+#pragma unroll
+            for (int k = 0; k < BATCH; ++k) acc += (q0 + k * kWaves < p.nseg) ? v[k] : 0.0;
+        }
+        red[wave][lane] = acc;
+        __syncthreads();
+        if (wave == 0 && i < p.m) {
+            const double s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+            out[i] = s;
+            if (mode == 1) {
+                rs = fma(p.r[i], s, rs);
+                ss = fma(s, s, ss);
             }
         }
-        return;
+        __syncthreads();
     }
-    if (mode != 1) return;
-    if (wave == 0) {
-        double rs = (i < p.m) ? p.r[i] * s : 0.0;
-        double ss = s * s;
+    if (mode == 1 && wave == 0) {
         rs = wave_sum(rs);
         ss = wave_sum(ss);
         if (lane == 0) {
-            st_agent(p.parts2 + 2ll * blockIdx.x, rs);
-            st_agent(p.parts2 + 2ll * blockIdx.x + 1, ss);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned long long old = __hip_atomic_fetch_add(&p.st->cnt_rowreduce, 1ull, __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT);
-            am_last = ((old + 1) % gridDim.x) == 0;
+            p.parts2[2ll * blockIdx.x] = rs;
+            p.parts2[2ll * blockIdx.x + 1] = ss;
         }
     }
-    __syncthreads();
-    if (!am_last) return;
-    // last arriver: every other block's partials are visible (sc1 stores drained before its add)
+    if (mode == 2 && blockIdx.x == 0) {
+        double a, b, e;
+        fold_parts(p, p.nparts, a, b, e);
+        if (threadIdx.x == 0) {
+            out[p.m] = a;
+            out[p.m + 1] = b;
+            for (int r = 0; r < p.nranks; ++r) out[p.m + 2 + r] = (r == p.rank) ? e : 0.0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// linesearch (one rank): fold the rowreduce and shrink partials in a fixed
+// order and run the line search + stopping rule.  One block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_linesearch(Params p, int nblocks_rr) {
+    if (p.st->done) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double rs = 0.0, ss = 0.0;
-    {
-        __shared__ double sr[kWaves], sq[kWaves];
-        for (int k = threadIdx.x; k < (int)gridDim.x; k += kThreads) {
-            rs += ld_agent(p.parts2 + 2ll * k);
-            ss += ld_agent(p.parts2 + 2ll * k + 1);
-        }
-        rs = wave_sum(rs);
-        ss = wave_sum(ss);
-        if (lane == 0) { sr[wave] = rs; sq[wave] = ss; }
-        __syncthreads();
-        rs = ((sr[0] + sr[1]) + sr[2]) + sr[3];
-        ss = ((sq[0] + sq[1]) + sq[2]) + sq[3];
+#pragma unroll 8
+    for (int k = threadIdx.x; k < nblocks_rr; k += kThreads) {
+        rs += p.parts2[2ll * k];
+        ss += p.parts2[2ll * k + 1];
     }
+    __shared__ double sr[kWaves], sq[kWaves];
+    rs = wave_sum(rs);
+    ss = wave_sum(ss);
+    if (lane == 0) { sr[wave] = rs; sq[wave] = ss; }
+    __syncthreads();
+    rs = ((sr[0] + sr[1]) + sr[2]) + sr[3];
+    ss = ((sq[0] + sq[1]) + sq[2]) + sq[3];
     double a, b, e;
     fold_parts(p, p.nparts, a, b, e);
     if (threadIdx.x == 0) finish_step(p, rs, ss, a, b, e);
