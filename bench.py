@@ -263,8 +263,9 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": kname + (" (A^T s11 pass + segment-finisher shrink)" if dom == "colpass"
-                               else " (A D pass + row-chunk finishers + line search)"),
+            "kernel": kname + ({"k_iter_a": " (A^T s11 pass + segment-finisher shrink)",
+                                "k_iter_b": " (A D pass + row-chunk finishers + line search)",
+                                "k_colpass": " (A^T s11 pass)", "k_rowpass": " (A D pass)"}[kname]),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
