@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=20190325)
     ap.add_argument("--fused", type=int, default=0, help="1: two-launch fused iteration; 0 (default): five kernels")
+    ap.add_argument("--rhs", type=int, default=1,
+                    help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
+    ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
     return ap.parse_args()
 
 
@@ -213,8 +216,95 @@ def pmc_traffic(workload_key, kernel):
         return None
 
 
+MFMA_BF16_DENSE_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def panel_bytes_pass(m, w, k):
+    """One MFMA pass of the panel path: A_b in bf16 (m x w) once, the k-wide
+    operand panel in (hi+lo bf16) and the fp32 split-K output once."""
+    return 2 * m * w + 4 * k * (m + w) + 4 * k * (m + w)
+
+
+def main_panel(args):
+    """configs[4]: k right-hand sides on m x n bf16 A (PanelLasso, MFMA passes)."""
+    import numpy as np
+    import torch
+    from convex_optimization_amd.panel import PanelLasso
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--rhs > 1 runs on one GPU (replicas only)")
+    torch.cuda.set_device(0)
+    m, n, k = args.m, args.n_per_gpu, args.rhs
+    g = torch.Generator(device="cuda").manual_seed(args.seed)
+    A = torch.randn(m, n, device="cuda", generator=g)
+    A /= A.norm(dim=1, keepdim=True)
+    Xt = torch.randn(n, k, device="cuda", generator=g) * (torch.rand(n, k, device="cuda", generator=g) < 0.4)
+    pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks)
+    del A
+    Ab = pl.A_bf16.float()
+    B = (Ab @ Xt + 0.01 * torch.randn(m, k, device="cuda", generator=g)).double()
+    mu = (0.1 * (Ab.t() @ B.float()).abs().amax(dim=0)).double().cpu().numpy()
+    del Ab
+    torch.cuda.synchronize()
+
+    def window(graph):
+        pl.solver_reset(B, mu, use_graph=graph)
+        pl.set_kernel_timing(not graph)
+        pl.solver_step(args.warmup)
+        pl.stream.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pl.solver_step(args.steps)
+        pl.stream.synchronize()
+        el = time.perf_counter() - t0
+        return el
+
+    el_graph = window(True)
+    st = pl.solver_status()
+    el_ev = window(False)
+    kms, samples = pl.kernel_times()
+    pl.set_kernel_timing(False)
+    w = pl.MAT_WIDTH
+    dom = max(("pass1_mfma", "pass2_mfma"), key=lambda q: kms[q])
+    pb = panel_bytes_pass(m, w, k)
+    achieved = pb / (kms[dom] * 1e-3) / 1e9
+    flops = 2 * m * w * k * 2                                    # hi + lo operand halves
+    tflops = flops / (kms[dom] * 1e-3) / 1e12
+    iters_s = args.steps / el_graph
+    alg_iter = 2 * pb
+    out = {
+        "metric": METRIC.replace("fp32", "bf16") + f", {k} right-hand sides",
+        "value": iters_s, "unit": f"iters/s ({k} right-hand sides per iteration)",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": el_graph / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16 (A) x split-bf16 operands, fp32 MFMA accumulate, fp64 reduce",
+        "data": "synthetic (A ~ N(0,1) rows unit-norm, bf16 in HBM; X_true density 0.4; B = A X_true + 0.01 E)",
+        "config": {
+            "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
+            "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
+            "alg_bytes_per_iter": alg_iter,
+            "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
+            "iter_roofline_frac": iters_s * alg_iter / (HBM_PEAK_GBS * 1e9),
+            "rhs_iters_per_s": iters_s * k,
+            "iters_per_s_eager_with_events": args.steps / el_ev,
+            "kernel_avg_ms": kms, "status": st,
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": {"pass1_mfma": "k_panel_pass1 (A^T R panel GEMM + shrink)",
+                                       "pass2_mfma": "k_panel_pass2 (A D panel GEMM)"}[dom],
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": pmc_traffic(f"panel_m{m}_n{n}_k{k}", dom), "alg_bytes_per_launch": pb,
+            "avg_launch_ms": kms[dom],
+            "mfma": {"achieved_tflops": tflops, "peak_tflops": MFMA_BF16_DENSE_TFLOPS,
+                     "frac": tflops / MFMA_BF16_DENSE_TFLOPS, "flops_per_launch": flops},
+        },
+    }
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
+    if args.rhs > 1:
+        return main_panel(args)
     import torch
     ctx = Ctx(args.gpus)
     G = ctx.world

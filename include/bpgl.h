@@ -178,6 +178,37 @@ int bpgl_set_tuning(bpgl_ctx* ctx, const char* key, int64_t value);
 int bpgl_geometry(const bpgl_ctx* ctx, int32_t* nseg, int32_t* nchunk, int32_t* rows_per_chunk,
                   int32_t* seg_width);
 
+/* ===========================================================================
+ * Panel path (BASELINE configs[4]): nrhs in {16, 32, 64, 128} right-hand sides
+ * solved together, A stored bf16 twice (row-major A [m][lda] and its transpose
+ * At [n][ldt], both caller-owned), both passes on CDNA4 MFMA
+ * (v_mfma_f32_16x16x32_bf16) with hi+lo bf16 split operands.  The reference
+ * has no batched solver: each RHS follows the single-RHS iteration of
+ * lasso.py:102-157 (cyclic blocks, fixed iteration count).  m and the block
+ * width must be multiples of 128.  Layouts: B, R [nrhs][m]; G, D [nrhs][w];
+ * x [nblock][nrhs][w] fp32.
+ * =========================================================================== */
+typedef struct bpgl_panel bpgl_panel;
+int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_t nblock, int32_t nrhs,
+                      int32_t kchunks /* <= 0: automatic */, void* hip_stream);
+void bpgl_panel_destroy(bpgl_panel* ctx);
+int64_t bpgl_panel_scratch_bytes(const bpgl_panel* ctx);
+int bpgl_panel_bind(bpgl_panel* ctx, const void* A, int64_t lda, const void* At, int64_t ldt, void* scratch,
+                    int64_t scratch_bytes);
+int bpgl_panel_diag(bpgl_panel* ctx, double* out /* nullable, n fp64 */);
+/* G = A_b^T R  and  S = A_b D  (fp64 in/out, device; split-bf16 MFMA inside) */
+int bpgl_panel_mtm(bpgl_panel* ctx, int32_t block, const double* R, double* G);
+int bpgl_panel_mm(bpgl_panel* ctx, int32_t block, const double* D, double* S);
+int bpgl_panel_reset(bpgl_panel* ctx, const double* B, const double* mu /* nrhs */, double* err_iter,
+                     int64_t record_len, int use_graph);
+int bpgl_panel_step(bpgl_panel* ctx, int64_t n_iter);
+int bpgl_panel_status(bpgl_panel* ctx, int64_t* iters, double* last_err);
+const float* bpgl_panel_x(bpgl_panel* ctx);
+int bpgl_panel_set_kernel_timing(bpgl_panel* ctx, int enable);
+int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce, step, update */,
+                            int64_t* samples);
+int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,7 @@ import os
 import pytest
 
 from convex_optimization_amd import _native as N
+from convex_optimization_amd import panel  # noqa: F401  (registers the bpgl_panel_* signatures)
 
 
 def test_library_present_and_loads():

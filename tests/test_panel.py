@@ -1,0 +1,106 @@
+"""Panel path (BASELINE configs[4]): k right-hand sides, bf16 A, CDNA4 MFMA.
+
+Oracle: the per-RHS C restatement (oracle_run) on the same bf16-rounded A in
+fp64.  Stated tolerance for this path (split-bf16 MFMA operands, fp32
+accumulation inside a tile): x within 1e-2 relative l2 of the oracle, the
+objective within 1e-5 relative; the two GEMMs within 1e-4 relative
+(max-norm) of fp64 products on the same bf16 A.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from convex_optimization_amd.panel import PanelLasso  # noqa: E402
+
+NT = min(16, os.cpu_count() or 1)
+
+
+def bf16_round(A):
+    return torch.from_numpy(np.ascontiguousarray(A, dtype=np.float32)).to(torch.bfloat16).to(torch.float64).numpy()
+
+
+def instance(m, n, k, seed=0):
+    rs = np.random.RandomState(seed)
+    A = rs.randn(m, n)
+    A /= np.linalg.norm(A, axis=1, keepdims=True)
+    Ab = bf16_round(A)
+    X = rs.randn(n, k) * (rs.rand(n, k) < 0.4)
+    B = Ab @ X + 0.01 * rs.randn(m, k)
+    mu = 0.1 * np.abs(Ab.T @ B).max(axis=0)
+    return Ab, B, mu
+
+
+@pytest.mark.parametrize("m,n,blocks,k", [(512, 2048, 1, 32), (256, 1024, 2, 16), (384, 768, 3, 64),
+                                          (128, 512, 1, 128)])
+def test_panel_gemms_match_fp64(m, n, blocks, k):
+    Ab, _, _ = instance(m, n, k, seed=m + n)
+    pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
+    w = n // blocks
+    np.testing.assert_allclose(pl.diag_ATA.reshape(-1), np.square(Ab).sum(axis=0), rtol=1e-12)
+    rs = np.random.RandomState(1)
+    R = rs.randn(m, k)
+    D = rs.randn(w, k)
+    for b in range(blocks):
+        Ablk = Ab[:, b * w:(b + 1) * w]
+        G = pl.mat_tMulMat(R, b).cpu().numpy()
+        ref = Ablk.T @ R
+        assert np.abs(G - ref).max() <= 1e-4 * np.abs(ref).max(), np.abs(G - ref).max() / np.abs(ref).max()
+        S = pl.matMulMat(D, b).cpu().numpy()
+        ref = Ablk @ D
+        assert np.abs(S - ref).max() <= 1e-4 * np.abs(ref).max(), np.abs(S - ref).max() / np.abs(ref).max()
+
+
+def objective(A, b, mu, x):
+    r = A @ x - b
+    return 0.5 * r @ r + mu * np.abs(x).sum()
+
+
+@pytest.mark.parametrize("m,n,blocks,k,iters", [(512, 2048, 1, 32, 150), (256, 1024, 2, 16, 120),
+                                                (384, 768, 3, 64, 90)])
+def test_panel_solver_matches_per_rhs_oracle(m, n, blocks, k, iters):
+    Ab, B, mu = instance(m, n, k, seed=7 + k)
+    pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
+    res = pl.run(B, mu, iters, record=True)
+    assert res["iters"] == iters
+    X = res["x"]
+    worst_x, worst_f = 0.0, 0.0
+    for j in range(k):
+        ref = oracle.run(Ab, B[:, j], mu[j], blocks, iters, nthreads=NT)["x"]
+        worst_x = max(worst_x, np.linalg.norm(X[:, j] - ref) / np.linalg.norm(ref))
+        f_dev, f_ref = objective(Ab, B[:, j], mu[j], X[:, j]), objective(Ab, B[:, j], mu[j], ref)
+        worst_f = max(worst_f, abs(f_dev - f_ref) / f_ref)
+    print(f"panel m={m} n={n} k={k}: worst rel x {worst_x:.2e}, worst rel objective {worst_f:.2e}")
+    assert worst_x <= 1e-2
+    assert worst_f <= 1e-5
+    assert np.all(np.isfinite(res["err_iter"]))
+
+
+def test_panel_graph_equals_eager_and_objective_decreases():
+    Ab, B, mu = instance(256, 1024, 16, seed=3)
+    pl = PanelLasso(Ab, 1, nrhs=16, device=0)
+    a = pl.run(B, mu, 40, use_graph=True)["x"]
+    b = pl.run(B, mu, 40, use_graph=False)["x"]
+    np.testing.assert_array_equal(a, b)
+    pl.solver_reset(B, mu)
+    prev = [objective(Ab, B[:, j], mu[j], np.zeros(1024)) for j in range(16)]
+    for _ in range(10):
+        pl.solver_step(3)
+        x = pl.solver_x()
+        cur = [objective(Ab, B[:, j], mu[j], x[:, j]) for j in range(16)]
+        assert all(c <= p * (1 + 1e-6) for c, p in zip(cur, prev))
+        prev = cur
+
+
+def test_panel_rejects_bad_shapes():
+    with pytest.raises(Exception):
+        PanelLasso(np.ones((100, 256)), 1, nrhs=16)
+    with pytest.raises(Exception):
+        PanelLasso(np.ones((128, 256)), 1, nrhs=24)
