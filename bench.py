@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--rhs", type=int, default=1,
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
+    ap.add_argument("--interleave", type=int, default=1, help="panel path: LDS-DMA spread over MFMA groups")
     return ap.parse_args()
 
 
@@ -239,6 +240,7 @@ def main_panel(args):
     A /= A.norm(dim=1, keepdim=True)
     Xt = torch.randn(n, k, device="cuda", generator=g) * (torch.rand(n, k, device="cuda", generator=g) < 0.4)
     pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks)
+    pl.set_tuning("interleave", args.interleave)
     del A
     Ab = pl.A_bf16.float()
     B = (Ab @ Xt + 0.01 * torch.randn(m, k, device="cuda", generator=g)).double()
@@ -281,6 +283,7 @@ def main_panel(args):
         "config": {
             "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
+            "interleave": args.interleave,
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
             "iter_roofline_frac": iters_s * alg_iter / (HBM_PEAK_GBS * 1e9),

@@ -792,6 +792,7 @@ struct bpgl_panel {
     bool timing = false;
     std::vector<hipEvent_t> evs;
     int64_t timed_iters = 0;
+    int interleave = 1;   // LDS-DMA pieces spread over the MFMA groups (tuning knob)
 };
 
 namespace {
@@ -826,31 +827,39 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     return L;
 }
 
-template <int NT>
+template <int NT, int ILV>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    const dim3 b(kThreads);
+    const dim3 b(PanelGeo<NT>::T);
     switch (which) {
         case 0:
-            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1>), dim3((unsigned)(c->w / kPanelRows)), b, 0, c->stream,
-                                         c->p, fixed_block, out);
-            else hipLaunchKernelGGL((k_panel_pass1<NT, 0>), dim3((unsigned)(c->w / kPanelRows)), b, 0, c->stream,
-                                    c->p, fixed_block, out);
+            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV>), dim3((unsigned)(c->w / kPanelRows)), b, 0,
+                                         c->stream, c->p, fixed_block, out);
+            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV>), dim3((unsigned)(c->w / kPanelRows)), b, 0,
+                                    c->stream, c->p, fixed_block, out);
             LAUNCH_CHECK("k_panel_pass1");
             break;
         case 1:
-            hipLaunchKernelGGL((k_panel_pass2<NT>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)), b, 0,
+            hipLaunchKernelGGL((k_panel_pass2<NT, ILV>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)), b, 0,
                                c->stream, c->p, fixed_block);
             LAUNCH_CHECK("k_panel_pass2");
             break;
     }
     return 0;
 }
+template <int NT>
+int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
+    switch (c->interleave) {
+        case 0: return panel_launch_nt<NT, 0>(c, which, fixed_block, out, mode);
+        case 1: return panel_launch_nt<NT, 1>(c, which, fixed_block, out, mode);
+        default: return panel_launch_nt<NT, 2>(c, which, fixed_block, out, mode);
+    }
+}
 int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (c->k) {
-        case 16: return panel_launch_nt<1>(c, which, fixed_block, out, mode);
-        case 32: return panel_launch_nt<2>(c, which, fixed_block, out, mode);
-        case 64: return panel_launch_nt<4>(c, which, fixed_block, out, mode);
-        default: return panel_launch_nt<8>(c, which, fixed_block, out, mode);
+        case 16: return panel_launch_ilv<1>(c, which, fixed_block, out, mode);
+        case 32: return panel_launch_ilv<2>(c, which, fixed_block, out, mode);
+        case 64: return panel_launch_ilv<4>(c, which, fixed_block, out, mode);
+        default: return panel_launch_ilv<8>(c, which, fixed_block, out, mode);
     }
 }
 int panel_reduce(bpgl_panel* c, double* out, int mode) {
@@ -919,11 +928,11 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
                                               kPanelRows);
     if (w <= 0 || w % kPanelRows) return fail(BPGL_E_ARG, "block width (%lld) must be a positive multiple of %d",
                                               (long long)w, kPanelRows);
-    if (kchunks <= 0) {   // ~1024 pass-2 tiles, chunk width a multiple of 128
-        kchunks = (int32_t)std::max<int64_t>(1, std::min<int64_t>(w / kPanelRows, 1024 / (m / kPanelRows)));
-        while (w % ((int64_t)kchunks * kPanelRows)) --kchunks;
+    if (kchunks <= 0) {   // one pass-2 tile per CU (256), chunk width a multiple of the 64-deep stage
+        kchunks = (int32_t)std::max<int64_t>(1, std::min<int64_t>(w / kPanelK, 256 / (m / kPanelRows)));
+        while (w % ((int64_t)kchunks * kPanelK)) --kchunks;
     }
-    if (w % ((int64_t)kchunks * kPanelRows)) return fail(BPGL_E_ARG, "w must be a multiple of 128 * kchunks");
+    if (w % ((int64_t)kchunks * kPanelK)) return fail(BPGL_E_ARG, "w must be a multiple of 64 * kchunks");
     HIP_TRY(hipSetDevice(device));
     bpgl_panel* c = new bpgl_panel();
     c->device = device;
@@ -957,14 +966,12 @@ void bpgl_panel_destroy(bpgl_panel* c) {
 
 int64_t bpgl_panel_scratch_bytes(const bpgl_panel* c) { return c ? panel_layout(c).total : -1; }
 
-int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, const void* At, int64_t ldt, void* scratch,
-                    int64_t scratch_bytes) {
+int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, int64_t scratch_bytes) {
     if (!c) return fail(BPGL_E_ARG, "null panel context");
-    if (!A || !At || !scratch) return fail(BPGL_E_ARG, "A, At and scratch must be non-null");
-    if (((uintptr_t)A) % 16 || ((uintptr_t)At) % 16) return fail(BPGL_E_ARG, "A and At must be 16-byte aligned");
+    if (!A || !scratch) return fail(BPGL_E_ARG, "A and scratch must be non-null");
+    if (((uintptr_t)A) % 16) return fail(BPGL_E_ARG, "A must be 16-byte aligned");
     if (((uintptr_t)scratch) % 256) return fail(BPGL_E_ARG, "scratch must be 256-byte aligned");
     if (lda < c->n || lda % 8) return fail(BPGL_E_ARG, "lda must be >= n and a multiple of 8");
-    if (ldt < c->m || ldt % 8) return fail(BPGL_E_ARG, "ldt must be >= m and a multiple of 8");
     const PanelLayout L = panel_layout(c);
     if (scratch_bytes < L.total) return fail(BPGL_E_SCRATCH, "scratch too small: %lld < %lld",
                                              (long long)scratch_bytes, (long long)L.total);
@@ -972,9 +979,7 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, const void* At, i
     PanelParams& p = c->p;
     p = PanelParams{};
     p.A = (const __bf16*)A;
-    p.At = (const __bf16*)At;
     p.lda = lda;
-    p.ldt = ldt;
     p.m = c->m;
     p.w = c->w;
     p.nblock = c->nblock;
@@ -1011,7 +1016,7 @@ int bpgl_panel_diag(bpgl_panel* c, double* out) {
     int rc;
     if ((rc = panel_ready(c))) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    hipLaunchKernelGGL(k_panel_diag, dim3((unsigned)cdiv(c->n, kWaves)), dim3(kThreads), 0, c->stream, c->p,
+    hipLaunchKernelGGL(k_panel_diag, dim3((unsigned)cdiv(c->n, 512)), dim3(kThreads), 0, c->stream, c->p,
                        const_cast<double*>(c->p.diag), const_cast<double*>(c->p.rec));
     LAUNCH_CHECK("k_panel_diag");
     if (out) HIP_TRY(hipMemcpyAsync(out, c->p.diag, 8 * c->n, hipMemcpyDeviceToDevice, c->stream));
@@ -1133,6 +1138,18 @@ int bpgl_panel_kernel_times(bpgl_panel* c, double* avg_ms /* 5 */, int64_t* samp
     for (int k = 0; k < kPanelKinds; ++k) avg_ms[k] = c->timed_iters ? sum[k] / c->timed_iters : 0.0;
     if (samples) *samples = c->timed_iters;
     c->timed_iters = 0;
+    return 0;
+}
+
+int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
+    if (!c || !key) return fail(BPGL_E_ARG, "null argument");
+    if (!strcmp(key, "interleave")) {
+        if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
+        c->interleave = (int)value;
+    } else {
+        return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
+    }
+    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
     return 0;
 }
 

@@ -9,20 +9,22 @@
 //   gamma_j = clip(-(r_j.s_j + mu_j(|Bx_j|_1 - |x_j|_1)) / |s_j|^2, 0, 1)   per RHS
 //   x_j += gamma_j D_j ;  Ax_j += gamma_j S_j ;  R = sum_b Ax_b - B
 //
-// Operands.  A is resident twice (row-major A for pass 2, its transpose At for
-// pass 1) so each pass loads its MFMA A-operand fragments straight from HBM as
-// 16-byte rows -- every A byte is still read once per pass.  R and D enter the
-// MFMA as hi + lo bf16 pairs (a ~16-bit mantissa); the direction actually used
+// Operands.  A is resident once, row-major bf16; every A byte is read once per
+// pass.  R and D enter the MFMA as hi + lo bf16 pairs (a ~16-bit mantissa); the direction actually used
 // is D' = Dh + Dl, with S = A D' and |x + D'|_1 in the line search, so the exact
 // line search of the reference still guarantees descent.  Accumulation: fp32
 // inside a block's MFMA chain, fp64 across pass-2 column chunks and in every
 // reduction after that.
 //
-// Tiles.  A wave owns 32 rows of its output (2 MFMA M-tiles of 16) for all k
-// RHS (NT = k/16 N-tiles); a block is 4 waves = 128 output rows.  The k-wide
-// operand tile of each 32-deep K step (hi and lo) is staged once per block in
-// LDS (double-buffered, registers -> LDS) and read with ds_read_b128; the A
-// fragments stream from HBM through a PF-deep register ring.
+// Tiles.  A block owns 256 output rows x all k RHS: 4 (M) x WN (N) waves, each
+// 64 rows (4 MFMA M-tiles) x k/WN RHS.  K advances 64 per stage.  Both operand
+// tiles of a stage travel HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4,
+// full 128-B lines, XOR-swizzled through the source address); the A side is
+// triple-buffered (two stages in flight), the k-wide side double-buffered, and
+// one raw s_barrier per stage orders both (counted vmcnt, never 0 in the loop).
+// Only row-major A is resident: pass 2 reads A fragments with ds_read_b128,
+// pass 1 (which needs A^T) reads the same kind of image with the CDNA4
+// transposing ds_read_b64_tr_b16.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -33,10 +35,26 @@ namespace bpgl {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kPanelRows = 128;   // output rows per block (4 waves x 32)
-constexpr int kPanelK = 32;       // K depth per MFMA step
-constexpr int kPanelPad = 40;     // LDS row length (elements) of a staged K step: 80 B
-constexpr int kPanelPF = 4;       // A-fragment prefetch depth (K steps)
+constexpr int kPanelRows = 256;   // output rows per block (pass 1: A columns, pass 2: A rows)
+constexpr int kPanelK = 64;       // K depth per stage
+constexpr int kPanelNA = 3;       // A-side stage buffers (two stages in flight)
+constexpr int kPanelNO = 2;       // k-wide-side stage buffers
+constexpr int kPanelAStage = kPanelRows * kPanelK * 2;   // 32 KiB
+
+template <int NT>
+struct PanelGeo {
+    static constexpr int WN = NT >= 2 ? 2 : 1;        // waves along the RHS
+    static constexpr int NTW = NT / WN;               // N-tiles per wave
+    static constexpr int NW = 4 * WN;                 // waves per block
+    static constexpr int T = 64 * NW;                 // threads per block
+    static constexpr int K = 16 * NT;                 // right-hand sides
+    static constexpr int OStage = 2 * K * kPanelK * 2;            // hi + lo rows of 128 B
+    static constexpr int LA = kPanelAStage / (T * 16);            // LDS-DMA per thread per A stage
+    static constexpr int LO = OStage / (T * 16);                  // ... per k-wide stage
+    static constexpr int Smem = kPanelNA * kPanelAStage + kPanelNO * OStage;
+    static_assert(LA >= 1 && LO >= 1, "stage must cover every thread");
+    static_assert(Smem <= 160 * 1024, "LDS budget");
+};
 
 struct PanelState {
     long long t;        // next iteration
@@ -48,8 +66,7 @@ struct PanelState {
 
 struct PanelParams {
     const __bf16* A;    // [m][lda]   block b at column offset b * w
-    const __bf16* At;   // [n][ldt]   block b at row offset b * w
-    long long lda, ldt;
+    long long lda;
     long long m, w;
     int nblock, k;
     int kchunks;        // pass-2 split of the block's w columns
@@ -77,100 +94,286 @@ struct PanelParams {
 
 constexpr int kLspRows = 1024;    // rows per line-search partial
 
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ __bf16 to_bf16(float v) { return (__bf16)v; }
 
-// stage one K step of a [k][len] bf16 hi/lo operand pair into LDS buffer `buf`:
-// elements [hl][rhs][0..31] <- src_hl[rhs * ld + k0 + 0..31]
-template <int NT>
-__device__ __forceinline__ void panel_stage_load(const __bf16* __restrict__ hi, const __bf16* __restrict__ lo,
-                                                 long long ld, long long k0, uint4 (&regs)[NT]) {
-    // 2 (hi/lo) x k rows x 4 sixteen-byte parts = 8k chunks; 256 threads -> NT chunks each (k = 16 NT)
-#pragma unroll
-    for (int s = 0; s < NT; ++s) {
-        const int c = threadIdx.x + kThreads * s;
-        const int hl = c / (64 * NT);
-        const int rem = c % (64 * NT);
-        const int rhs = rem >> 2, part = rem & 3;
-        const __bf16* src = (hl ? lo : hi) + (long long)rhs * ld + k0 + part * 8;
-        regs[s] = *reinterpret_cast<const uint4*>(src);
-    }
+// one LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to lds_base + 16 * lane
+__device__ __forceinline__ void glds16(const void* src, char* lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)lds_base, 16, 0, 0);
 }
-template <int NT>
-__device__ __forceinline__ void panel_stage_store(__bf16* lds, int buf, const uint4 (&regs)[NT]) {
-#pragma unroll
-    for (int s = 0; s < NT; ++s) {
-        const int c = threadIdx.x + kThreads * s;
-        const int hl = c / (64 * NT);
-        const int rem = c % (64 * NT);
-        const int rhs = rem >> 2, part = rem & 3;
-        __bf16* dst = lds + ((long long)((buf * 2 + hl) * (16 * NT) + rhs)) * kPanelPad + part * 8;
-        *reinterpret_cast<uint4*>(dst) = regs[s];
-    }
-}
-// B fragment (16x16x32 layout: lane l holds B[k = 8(l>>4)+j][n = l&15])
-template <int NT>
-__device__ __forceinline__ bf16x8 panel_bfrag(const __bf16* lds, int buf, int hl, int nt, int lane) {
-    const __bf16* p = lds + ((long long)((buf * 2 + hl) * (16 * NT) + nt * 16 + (lane & 15))) * kPanelPad +
-                      8 * (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(p);
+// all but the youngest N vector-memory ops of this wave done, LDS reads retired, then barrier
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-// One block-tile GEMM: acc[mt][nt] (rows = this wave's 32 output rows, cols = k RHS)
-//   = sum over K steps s of  Arows[row][K0 + 32 s + ...] . (Bh + Bl)[rhs][K0 + 32 s + ...]
-// Arows: row-major bf16 operand whose row `r` starts at arow_base + r * ldarow.
+// Image with 128-B rows (8 chunks of 16 B): chunk c of row r sits at 16 * (c ^ ((r >> 1) & 7)).
+// ds_read_b128 of a 16x16x32 fragment (row = lane & 15, chunk = lane >> 4 (+4)) is conflict-free.
+__device__ __forceinline__ int swz128(int r, int c) { return c ^ ((r >> 1) & 7); }
+// Image with 512-B rows (32 chunks) read by ds_read_b64_tr_b16: chunk c of row r at
+// 16 * (c ^ 2 * ((r & 3) | ((r >> 3 & 1) << 2))): the 8 rows of a 32-lane half land on
+// 8 distinct 32-B bank groups.
+__device__ __forceinline__ int swz512(int r, int c) { return c ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2))); }
+
+// k-wide operand stage: [hl][k][64] bf16 from hi/lo [k][ld] at column ks, piece q of this
+// wave (a piece = 8 image rows of 128 B)
 template <int NT>
-__device__ __forceinline__ void panel_gemm(const __bf16* __restrict__ arow_base, long long ldarow,
-                                           const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
-                                           long long ldb, long long K0, int nsteps, __bf16* lds,
-                                           f32x4 (&acc)[2][NT]) {
+__device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__ hi, const __bf16* __restrict__ lo,
+                                               long long ld, long long ks, char* obuf, int wave, int lane) {
+    using G = PanelGeo<NT>;
+    const int pc = q * G::NW + wave;
+    const int rr = pc * 8 + (lane >> 3);
+    const int c = swz128(rr, lane & 7);
+    const int hl = rr / G::K, rhs = rr % G::K;
+    glds16((hl ? lo : hi) + (long long)rhs * ld + ks + 8 * c, obuf + pc * 1024);
+}
+// pass-1 A stage: rows ks..ks+63 of A, columns col0..col0+255 -> [64][512 B] (a piece = 2 rows)
+template <int NT>
+__device__ __forceinline__ void panel_a1_piece(int q, const __bf16* __restrict__ A, long long lda, long long ks,
+                                               long long col0, char* abuf, int wave, int lane) {
+    using G = PanelGeo<NT>;
+    const int pc = q * G::NW + wave;
+    const int row = pc * 2 + (lane >> 5);
+    const int c = swz512(row, lane & 31);
+    glds16(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
+}
+// pass-2 A stage: rows r0..r0+255 of A, columns ks..ks+63 -> [256][128 B] (a piece = 8 rows)
+template <int NT>
+__device__ __forceinline__ void panel_a2_piece(int q, const __bf16* __restrict__ A, long long lda, long long r0,
+                                               long long ks, char* abuf, int wave, int lane) {
+    using G = PanelGeo<NT>;
+    const int pc = q * G::NW + wave;
+    const int row = pc * 8 + (lane >> 3);
+    const int c = swz128(row, lane & 7);
+    glds16(A + (r0 + row) * lda + ks + 8 * c, abuf + pc * 1024);
+}
+
+// B fragment (lane: rhs = lane & 15 of the N-tile, K = 32h + 8(lane>>4) + 0..7)
+__device__ __forceinline__ bf16x8 panel_bfrag(const char* obuf, int rr, int h, int lane) {
+    return *reinterpret_cast<const bf16x8*>(obuf + rr * 128 + 16 * swz128(rr, 4 * h + (lane >> 4)));
+}
+// pass-2 A fragment: row of the [256][128 B] image
+__device__ __forceinline__ bf16x8 panel_afrag2(const char* abuf, int row, int h, int lane) {
+    return *reinterpret_cast<const bf16x8*>(abuf + row * 128 + 16 * swz128(row, 4 * h + (lane >> 4)));
+}
+// pass-1 A^T fragment from the [64][512 B] image: output row = column j0 + (lane & 15),
+// K = 32h + 8(lane>>4) + 0..7, two transposing reads of 4 K-rows each
+__device__ __forceinline__ bf16x8 panel_afrag1(const char* abuf, int j0, int h, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int c = (j0 >> 3) + (p >> 1);
+    const int r0 = 32 * h + 8 * g + q;
+    const int r1 = r0 + 4;
+    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(abuf + r0 * 512 + 16 * swz512(r0, c) + 8 * (p & 1)));
+    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(abuf + r1 * 512 + 16 * swz512(r1, c) + 8 * (p & 1)));
+    const s16x4 lohalf = v0, hihalf = v1;
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = __builtin_shufflevector(lohalf, hihalf, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// Block-tile GEMM over nsteps stages of 64:
+//   PASS 1: acc[mt][nt] += A[ks.., col0 + j]^T (Rh + Rl)[rhs][ks..]      (rows j, K = A rows)
+//   PASS 2: acc[mt][nt] += A[r0 + i][colk + ks..] (Dh + Dl)[rhs][ks..]   (rows i, K = A columns)
+// `a_row0`/`a_col0`: PASS 1 -> (first A row of K, first column of the tile); PASS 2 -> (first row, first column of K).
+// ILV 0: a stage's LDS-DMA pieces are issued together after the barrier; ILV 1: they
+// are spread over the stage's MFMA groups (one scheduling group each).
+template <int NT, int PASS, int ILV>
+__device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restrict__ A, long long lda,
+                                               long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
+                                               const __bf16* __restrict__ bl, long long ldb, long long b_k0,
+                                               int nsteps, f32x4 (&acc)[4][PanelGeo<NT>::NTW]) {
+    using G = PanelGeo<NT>;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    char* abufs = smem;
+    char* obufs = smem + kPanelNA * kPanelAStage;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // A fragment of M-tile mt at step s: row (wave*32 + mt*16 + (lane&15)), K (K0 + 32 s + 8(lane>>4))
-    const __bf16* ap[2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-        ap[mt] = arow_base + (long long)(wave * 32 + mt * 16 + (lane & 15)) * ldarow + K0 + 8 * (lane >> 4);
-    bf16x8 ring[kPanelPF][2];
-#pragma unroll
-    for (int u = 0; u < kPanelPF; ++u)
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) ring[u][mt] = *reinterpret_cast<const bf16x8*>(ap[mt] + u * kPanelK);
-    uint4 stage[NT];
-    panel_stage_load<NT>(bh, bl, ldb, K0, stage);
-    panel_stage_store<NT>(lds, 0, stage);
-    __syncthreads();
-    for (int s0 = 0; s0 < nsteps; s0 += kPanelPF) {
-#pragma unroll
-        for (int u = 0; u < kPanelPF; ++u) {
-            const int s = s0 + u;
-            const int buf = u & 1;               // kPanelPF even: parity of s
-            // stage the next step (the last step re-stages itself: no branch around the loads)
-            const int snext = (s + 1 < nsteps) ? s + 1 : s;
-            panel_stage_load<NT>(bh, bl, ldb, K0 + (long long)snext * kPanelK, stage);
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const bf16x8 b_hi = panel_bfrag<NT>(lds, buf, 0, nt, lane);
-                const bf16x8 b_lo = panel_bfrag<NT>(lds, buf, 1, nt, lane);
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[u][mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[u][mt], b_lo, acc[mt][nt], 0, 0, 0);
-                }
-            }
-            {
-                const int sr = (s + kPanelPF < nsteps) ? s + kPanelPF : s;   // clamp: no branch around loads
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
-                    ring[u][mt] = *reinterpret_cast<const bf16x8*>(ap[mt] + (long long)sr * kPanelK);
-            }
-            panel_stage_store<NT>(lds, buf ^ 1, stage);
-            __syncthreads();
+        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // piece i of stage (so, sa): i < LO -> k-wide piece, else A piece i - LO (this order is what
+    // the counted wait below assumes: the youngest LA operations are A pieces)
+    auto piece = [&](int i, int so, int bo, int sa, int ba) {
+        if (i < G::LO) {
+            panel_op_piece<NT>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave, lane);
+        } else if (PASS == 1) {
+            panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+                               abufs + ba * kPanelAStage, wave, lane);
+        } else {
+            panel_a2_piece<NT>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+                               abufs + ba * kPanelAStage, wave, lane);
         }
+    };
+    auto issue_a = [&](int s, int buf) {
+#pragma unroll
+        for (int i = G::LO; i < G::LO + G::LA; ++i) piece(i, 0, 0, s, buf);
+    };
+    auto issue_o = [&](int s, int buf) {
+#pragma unroll
+        for (int i = 0; i < G::LO; ++i) piece(i, s, buf, 0, 0);
+    };
+    constexpr int NP = G::LO + G::LA;
+    constexpr int NG = 2 * G::NTW;                 // MFMA groups per stage
+    constexpr int PPG = (NP + NG - 1) / NG;         // pieces per group (ILV)
+    // prologue: op(0), A(0), A(1) -- the loop's counted wait assumes exactly this issue order
+    issue_o(0, 0);
+    issue_a(0, 0);
+    issue_a(nsteps > 1 ? 1 : 0, 1);
+    int abuf = 0;
+    for (int s = 0; s < nsteps; ++s) {
+        // everything but A(s+1) has landed (op(s), A(s)); every wave is past stage s-1's reads
+        wait_vm_barrier<G::LA>();
+        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
+        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
+        if (!ILV) {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) piece(i, so, bo, sa, ba);
+        }
+        const char* ab = abufs + abuf * kPanelAStage;
+        const char* ob = obufs + (s & 1) * G::OStage;
+        static_for<0, 2>([&](auto hc) {
+            constexpr int h = decltype(hc)::value;
+            bf16x8 af[4];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+                af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
+                                   : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
+            static_for<0, G::NTW>([&](auto ntc) {
+                constexpr int nt = decltype(ntc)::value;
+                constexpr int grp = h * G::NTW + nt;
+                constexpr int p0 = grp * PPG < NP ? grp * PPG : NP;
+                constexpr int p1 = (grp + 1) * PPG < NP ? (grp + 1) * PPG : NP;
+                if constexpr (ILV) {
+                    static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
+                }
+                const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
+                const bf16x8 b_hi = panel_bfrag(ob, rhs, h, lane);
+                const bf16x8 b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
+                }
+                if constexpr (ILV) {
+                    if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
+                }
+            });
+        });
+        abuf = abuf == 2 ? 0 : abuf + 1;
     }
+    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
+}
+
+// Software-pipelined form of the same GEMM (interleave knob 2).  The stage barrier sits
+// before a stage's LAST MFMA group: the fragments of the next stage's first group are read
+// behind that group's MFMAs, and every group's fragments are read one group ahead.  Buffer
+// reuse is unchanged (a stage's buffers are refilled only after the barrier that follows
+// all of its reads); all LDS-DMA pieces of a stage are issued before its barrier, spread
+// over the first G - 1 groups.
+template <int NT, int PASS>
+__device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __restrict__ A, long long lda,
+                                                    long long a_row0, long long a_col0,
+                                                    const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
+                                                    long long ldb, long long b_k0, int nsteps,
+                                                    f32x4 (&acc)[4][PanelGeo<NT>::NTW]) {
+    using G = PanelGeo<NT>;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    char* abufs = smem;
+    char* obufs = smem + kPanelNA * kPanelAStage;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto piece = [&](int i, int so, int bo, int sa, int ba) {
+        if (i < G::LO) {
+            panel_op_piece<NT>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave, lane);
+        } else if (PASS == 1) {
+            panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+                               abufs + ba * kPanelAStage, wave, lane);
+        } else {
+            panel_a2_piece<NT>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+                               abufs + ba * kPanelAStage, wave, lane);
+        }
+    };
+    constexpr int NP = G::LO + G::LA;
+    constexpr int NG = 2 * G::NTW;                                  // MFMA groups per stage (h, nt)
+    constexpr int NGI = NG > 1 ? NG - 1 : 1;                        // groups that carry LDS-DMA pieces
+    constexpr int PPG = (NP + NGI - 1) / NGI;
+    auto read_a = [&](const char* ab, int h, bf16x8 (&af)[4]) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+            af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
+                               : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
+    };
+    auto read_b = [&](const char* ob, int h, int nt, bf16x8& bhi, bf16x8& blo) {
+        const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
+        bhi = panel_bfrag(ob, rhs, h, lane);
+        blo = panel_bfrag(ob, G::K + rhs, h, lane);
+    };
+
+    // prologue: op(0), A(0), A(1), then stage 0 landed and group 0's fragments read
+    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
+    wait_vm_barrier<G::LA>();
+    bf16x8 af[2][4];
+    bf16x8 bfr[2][2];
+    read_a(abufs, 0, af[0]);
+    read_b(obufs, 0, 0, bfr[0][0], bfr[0][1]);
+    int abuf = 0;
+    for (int s = 0; s < nsteps; ++s) {
+        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
+        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
+        const int abuf_next = abuf == 2 ? 0 : abuf + 1;
+        const char* ab = abufs + abuf * kPanelAStage;
+        const char* ob = obufs + (s & 1) * G::OStage;
+        static_for<0, NG>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            constexpr int h = g / G::NTW, nt = g % G::NTW;
+            constexpr int cb = g & 1, ca = h & 1;
+            constexpr int p0 = g < NGI ? (g * PPG < NP ? g * PPG : NP) : NP;
+            constexpr int p1 = g < NGI ? ((g + 1) * PPG < NP ? (g + 1) * PPG : NP) : NP;
+            static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
+            if constexpr (g + 1 < NG) {
+                constexpr int h1 = (g + 1) / G::NTW, nt1 = (g + 1) % G::NTW;
+                if constexpr (h1 != h) read_a(ab, h1, af[h1 & 1]);
+                read_b(ob, h1, nt1, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
+            } else {
+                // stage s + 1 landed (only A(s+2) may be outstanding); stage s's reads retired
+                wait_vm_barrier<G::LA>();
+                const char* abn = abufs + abuf_next * kPanelAStage;
+                const char* obn = obufs + ((s + 1) & 1) * G::OStage;
+                read_a(abn, 0, af[0]);   // the last group runs on af[1] (h = 1)
+                read_b(obn, 0, 0, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][0], acc[mt][nt], 0, 0, 0);
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][1], acc[mt][nt], 0, 0, 0);
+            }
+        });
+        abuf = abuf_next;
+    }
+    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
 __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
@@ -181,41 +384,49 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 
 // ---------------------------------------------------------------------------
 // pass 1: G = A_m^T R (EPI 0: write G [k][w] fp64 -- API), or the fused shrink
-// epilogue (EPI 1: D' split, norms per RHS).  grid = w / 128 blocks of 256.
+// epilogue (EPI 1: D' split, norms per RHS).  grid = w / 256 blocks.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI>
-__global__ __launch_bounds__(kThreads) void k_panel_pass1(PanelParams p, int fixed_block, double* __restrict__ Gout) {
-    __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 2 * 16 * NT * kPanelPad];
+template <int NT, int EPI, int ILV>
+__global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, int fixed_block,
+                                                                  double* __restrict__ Gout) {
+    using G = PanelGeo<NT>;
+    __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block
-    const __bf16* arow = p.At + ((long long)mb * p.w + c0) * p.ldt;      // At rows = A columns
-    f32x4 acc[2][NT];
-    panel_gemm<NT>(arow, p.ldt, p.Rh, p.Rl, p.m, 0, (int)(p.m / kPanelK), lds, acc);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
+    f32x4 acc[4][G::NTW];
+    if constexpr (ILV == 2)
+        panel_mainloop_pipe<NT, 1>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+                                   (int)(p.m / kPanelK), acc);
+    else
+        panel_mainloop<NT, 1, ILV>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+                                   (int)(p.m / kPanelK), acc);
 
     // C layout: row = (lane>>4)*4 + r (A column), col = lane & 15 (RHS)
     if (EPI == 0) {
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const int rhs = nt * 16 + (lane & 15);
-                const long long j = c0 + wave * 32 + mt * 16 + (lane >> 4) * 4;
+            for (int nt = 0; nt < G::NTW; ++nt) {
+                const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
+                const long long j = c0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) Gout[(long long)rhs * p.w + j + r] = (double)acc[mt][nt][r];
             }
         return;
     }
-    __shared__ double nred[kWaves][16 * NT][3];
+    double* nred = reinterpret_cast<double*>(smem);   // [4 wm][k][3]
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int rhs = nt * 16 + (lane & 15);
+    for (int nt = 0; nt < G::NTW; ++nt) {
+        const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
         const double mu = p.mu[rhs];
         double sbx = 0.0, sx = 0.0, err = 0.0;
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            const long long j = c0 + wave * 32 + mt * 16 + (lane >> 4) * 4;   // 4 consecutive columns
-            float* xp = p.X + ((long long)mb * p.k + rhs) * p.w + j;
+        for (int mt = 0; mt < 4; ++mt) {
+            const long long j = c0 + wm * 64 + mt * 16 + (lane >> 4) * 4;   // 4 consecutive columns
+            const float* xp = p.X + ((long long)mb * p.k + rhs) * p.w + j;
             const float4 x4 = *reinterpret_cast<const float4*>(xp);
             const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
             __bf16 dh[4], dl[4];
@@ -232,10 +443,9 @@ __global__ __launch_bounds__(kThreads) void k_panel_pass1(PanelParams p, int fix
                 const double e = fabs(g - proj(g - x, -mu, mu));
                 err = (e > err || e != e) ? e : err;
             }
-            __bf16* dhp = p.Dh + (long long)rhs * p.w + j;
-            __bf16* dlp = p.Dl + (long long)rhs * p.w + j;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { dhp[r] = dh[r]; dlp[r] = dl[r]; }
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4*>(p.Dh + (long long)rhs * p.w + j) = bf16x4{dh[0], dh[1], dh[2], dh[3]};
+            *reinterpret_cast<bf16x4*>(p.Dl + (long long)rhs * p.w + j) = bf16x4{dl[0], dl[1], dl[2], dl[3]};
         }
         // lanes l, l^16, l^32, l^48 share the RHS
         sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
@@ -243,19 +453,20 @@ __global__ __launch_bounds__(kThreads) void k_panel_pass1(PanelParams p, int fix
         { double o = __shfl_xor(err, 16); err = (o > err || o != o) ? o : err;
           o = __shfl_xor(err, 32); err = (o > err || o != o) ? o : err; }
         if (lane < 16) {
-            nred[wave][rhs][0] = sbx;
-            nred[wave][rhs][1] = sx;
-            nred[wave][rhs][2] = err;
+            double* d = nred + ((long long)wm * G::K + rhs) * 3;
+            d[0] = sbx;
+            d[1] = sx;
+            d[2] = err;
         }
     }
     __syncthreads();
-    for (int rhs = threadIdx.x; rhs < 16 * NT; rhs += kThreads) {
+    for (int rhs = threadIdx.x; rhs < G::K; rhs += G::T) {
         double a = 0.0, b = 0.0, e = 0.0;
-        for (int q = 0; q < kWaves; ++q) {
-            a += nred[q][rhs][0];
-            b += nred[q][rhs][1];
-            const double eq = nred[q][rhs][2];
-            e = (eq > e || eq != eq) ? eq : e;
+        for (int q = 0; q < 4; ++q) {
+            const double* d = nred + ((long long)q * G::K + rhs) * 3;
+            a += d[0];
+            b += d[1];
+            e = (d[2] > e || d[2] != d[2]) ? d[2] : e;
         }
         double* dst = p.norms + ((long long)blockIdx.x * p.k + rhs) * 4;
         dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
@@ -264,26 +475,44 @@ __global__ __launch_bounds__(kThreads) void k_panel_pass1(PanelParams p, int fix
 
 // ---------------------------------------------------------------------------
 // pass 2: partial S over one column chunk: Sslab[chunk][rhs][row]
-// grid = (m / 128) x kchunks
+// grid = (m / 256) x kchunks
 // ---------------------------------------------------------------------------
-template <int NT>
-__global__ __launch_bounds__(kThreads) void k_panel_pass2(PanelParams p, int fixed_block) {
-    __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 2 * 16 * NT * kPanelPad];
+template <int NT, int ILV>
+__global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, int fixed_block) {
+    using G = PanelGeo<NT>;
+    __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int rb = blockIdx.x % (int)(p.m / kPanelRows);
-    const int chunk = blockIdx.x / (int)(p.m / kPanelRows);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    const int nrb = (int)(p.m / kPanelRows);
+    // XCD-aware: blocks are dealt to the 8 XCDs round-robin (blockIdx % 8); when the chunk
+    // count allows, give all row blocks of a column chunk (which share its D panel) one XCD.
+    int rb = blockIdx.x % nrb, chunk = blockIdx.x / nrb;
+    if (p.kchunks % 8 == 0) {                          // kchunks / 8 chunks per XCD
+        const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+        chunk = xcd * (p.kchunks / 8) + slot / nrb;
+        rb = slot % nrb;
+    } else if (8 % p.kchunks == 0 && nrb % (8 / p.kchunks) == 0) {   // 8 / kchunks XCDs per chunk
+        const int xpc = 8 / p.kchunks, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+        chunk = xcd / xpc;
+        rb = (xcd % xpc) * (nrb / xpc) + slot;
+    }
     const long long kc = p.w / p.kchunks;
     const long long r0 = (long long)rb * kPanelRows;
-    const __bf16* arow = p.A + r0 * p.lda + (long long)mb * p.w;        // A rows, block mb columns
-    f32x4 acc[2][NT];
-    panel_gemm<NT>(arow, p.lda, p.Dh, p.Dl, p.w, chunk * kc, (int)(kc / kPanelK), lds, acc);
+    f32x4 acc[4][G::NTW];
+    if constexpr (ILV == 2)
+        panel_mainloop_pipe<NT, 2>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
+                                   chunk * kc, (int)(kc / kPanelK), acc);
+    else
+        panel_mainloop<NT, 2, ILV>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
+                                   chunk * kc, (int)(kc / kPanelK), acc);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            const int rhs = nt * 16 + (lane & 15);
-            const long long row = r0 + wave * 32 + mt * 16 + (lane >> 4) * 4;
+        for (int nt = 0; nt < G::NTW; ++nt) {
+            const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
+            const long long row = r0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
             float* dst = p.Sslab + ((long long)chunk * p.k + rhs) * p.m + row;
             *reinterpret_cast<float4*>(dst) = make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2],
                                                           acc[mt][nt][3]);
@@ -402,22 +631,30 @@ __global__ __launch_bounds__(kThreads) void k_panel_split(const double* __restri
     }
 }
 
-// diag(A_b^T A_b) from At rows: one wave per column
+// diag(A^T A) from row-major A: a block owns 512 columns (64 lanes x 8), its 4
+// waves take every 4th row; fixed-order fp64 combine.  grid = n / 512
 __global__ __launch_bounds__(kThreads) void k_panel_diag(PanelParams p, double* __restrict__ diag,
                                                          double* __restrict__ rec) {
-    const int lane = threadIdx.x & 63;
-    const long long col = (long long)blockIdx.x * kWaves + (threadIdx.x >> 6);
-    if (col >= (long long)p.nblock * p.w) return;
-    const __bf16* row = p.At + col * p.ldt;
-    double acc = 0.0;
-    for (long long i = lane; i < p.m; i += 64) {
-        const double v = (double)(float)row[i];
-        acc = fma(v, v, acc);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long n = (long long)p.nblock * p.w;
+    const long long col = (long long)blockIdx.x * 512 + lane * 8;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (long long i = wave; i < p.m && col < n; i += kWaves) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(p.A + i * p.lda + col);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const double d = (double)(float)v[e];
+            acc[e] = fma(d, d, acc[e]);
+        }
     }
-    acc = wave_sum(acc);
-    if (lane == 0) {
-        diag[col] = acc;
-        rec[col] = 1.0 / acc;
+    __shared__ double part[kWaves][512];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[wave][lane * 8 + e] = acc[e];
+    __syncthreads();
+    for (int c = threadIdx.x; c < 512 && blockIdx.x * 512LL + c < n; c += kThreads) {
+        const double s = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
+        diag[blockIdx.x * 512 + c] = s;
+        rec[blockIdx.x * 512 + c] = 1.0 / s;
     }
 }
 

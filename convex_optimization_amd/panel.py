@@ -29,7 +29,7 @@ _PANEL_SIGS = {
     "bpgl_panel_create": (ctypes.c_int, [ctypes.POINTER(_p), ctypes.c_int, _i64, _i64, _i32, _i32, _i32, _p]),
     "bpgl_panel_destroy": (None, [_p]),
     "bpgl_panel_scratch_bytes": (_i64, [_p]),
-    "bpgl_panel_bind": (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p, _i64]),
+    "bpgl_panel_bind": (ctypes.c_int, [_p, _p, _i64, _p, _i64]),
     "bpgl_panel_diag": (ctypes.c_int, [_p, _p]),
     "bpgl_panel_mtm": (ctypes.c_int, [_p, _i32, _p, _p]),
     "bpgl_panel_mm": (ctypes.c_int, [_p, _i32, _p, _p]),
@@ -40,6 +40,7 @@ _PANEL_SIGS = {
     "bpgl_panel_set_kernel_timing": (ctypes.c_int, [_p, ctypes.c_int]),
     "bpgl_panel_kernel_times": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "bpgl_panel_geometry": (ctypes.c_int, [_p, ctypes.POINTER(_i32)]),
+    "bpgl_panel_set_tuning": (ctypes.c_int, [_p, ctypes.c_char_p, _i64]),
 }
 N._SIGS.update(_PANEL_SIGS)
 
@@ -76,14 +77,12 @@ class PanelLasso:
         self._ctx = ctx
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
-            At_src = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))
-            self._A = At_src.to(device=self.device, dtype=torch.bfloat16).contiguous()     # [m][n]
-            self._At = self._A.t().contiguous()                                             # [n][m]
+            A_src = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))
+            self._A = A_src.to(device=self.device, dtype=torch.bfloat16).contiguous()     # [m][n]
             nbytes = int(L.bpgl_panel_scratch_bytes(ctx))
             self._scratch = torch.empty(nbytes // 8 + 64, dtype=torch.float64, device=self.device)
             base = (self._scratch.data_ptr() + 255) // 256 * 256
-            N.check(L.bpgl_panel_bind(ctx, ctypes.c_void_p(self._A.data_ptr()), K,
-                                      ctypes.c_void_p(self._At.data_ptr()), H, ctypes.c_void_p(base), nbytes),
+            N.check(L.bpgl_panel_bind(ctx, ctypes.c_void_p(self._A.data_ptr()), K, ctypes.c_void_p(base), nbytes),
                     "bpgl_panel_bind")
             self._diag = torch.empty(K, dtype=torch.float64, device=self.device)
             N.check(L.bpgl_panel_diag(ctx, N.ptr(self._diag)), "bpgl_panel_diag")
@@ -172,6 +171,10 @@ class PanelLasso:
     def solver_x(self):
         self.stream.synchronize()
         return self.solver_x_device().to(torch.float64).cpu().numpy().T.copy()   # (n, k)
+
+    def set_tuning(self, key, value):
+        """Speed-only knobs (bitwise-identical results): 'interleave' 0/1."""
+        N.check(_lib().bpgl_panel_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_panel_set_tuning")
 
     def set_kernel_timing(self, enable):
         N.check(_lib().bpgl_panel_set_kernel_timing(self._ctx, int(bool(enable))), "bpgl_panel_set_kernel_timing")

@@ -185,7 +185,7 @@ int bpgl_geometry(const bpgl_ctx* ctx, int32_t* nseg, int32_t* nchunk, int32_t* 
  * (v_mfma_f32_16x16x32_bf16) with hi+lo bf16 split operands.  The reference
  * has no batched solver: each RHS follows the single-RHS iteration of
  * lasso.py:102-157 (cyclic blocks, fixed iteration count).  m and the block
- * width must be multiples of 128.  Layouts: B, R [nrhs][m]; G, D [nrhs][w];
+ * width must be multiples of 256.  Layouts: B, R [nrhs][m]; G, D [nrhs][w];
  * x [nblock][nrhs][w] fp32.
  * =========================================================================== */
 typedef struct bpgl_panel bpgl_panel;
@@ -193,7 +193,7 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
                       int32_t kchunks /* <= 0: automatic */, void* hip_stream);
 void bpgl_panel_destroy(bpgl_panel* ctx);
 int64_t bpgl_panel_scratch_bytes(const bpgl_panel* ctx);
-int bpgl_panel_bind(bpgl_panel* ctx, const void* A, int64_t lda, const void* At, int64_t ldt, void* scratch,
+int bpgl_panel_bind(bpgl_panel* ctx, const void* A /* [m][lda] bf16 */, int64_t lda, void* scratch,
                     int64_t scratch_bytes);
 int bpgl_panel_diag(bpgl_panel* ctx, double* out /* nullable, n fp64 */);
 /* G = A_b^T R  and  S = A_b D  (fp64 in/out, device; split-bf16 MFMA inside) */
@@ -207,6 +207,11 @@ const float* bpgl_panel_x(bpgl_panel* ctx);
 int bpgl_panel_set_kernel_timing(bpgl_panel* ctx, int enable);
 int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce, step, update */,
                             int64_t* samples);
+/* tuning knobs (results are bitwise independent of them): "interleave" 0/1/2 --
+ * LDS-DMA pieces issued together after each stage barrier (0), spread over
+ * the stage's MFMA groups (1, default), or spread and software-pipelined with
+ * fragment reads one MFMA group ahead across the stage barrier (2). */
+int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
 
 #ifdef __cplusplus

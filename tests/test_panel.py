@@ -38,8 +38,8 @@ def instance(m, n, k, seed=0):
     return Ab, B, mu
 
 
-@pytest.mark.parametrize("m,n,blocks,k", [(512, 2048, 1, 32), (256, 1024, 2, 16), (384, 768, 3, 64),
-                                          (128, 512, 1, 128)])
+@pytest.mark.parametrize("m,n,blocks,k", [(512, 2048, 1, 32), (256, 1024, 2, 16), (768, 768, 3, 64),
+                                          (256, 512, 1, 128), (1024, 4096, 2, 128)])
 def test_panel_gemms_match_fp64(m, n, blocks, k):
     Ab, _, _ = instance(m, n, k, seed=m + n)
     pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
@@ -64,7 +64,7 @@ def objective(A, b, mu, x):
 
 
 @pytest.mark.parametrize("m,n,blocks,k,iters", [(512, 2048, 1, 32, 150), (256, 1024, 2, 16, 120),
-                                                (384, 768, 3, 64, 90)])
+                                                (768, 768, 3, 64, 90), (512, 1024, 1, 128, 60)])
 def test_panel_solver_matches_per_rhs_oracle(m, n, blocks, k, iters):
     Ab, B, mu = instance(m, n, k, seed=7 + k)
     pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
@@ -99,8 +99,23 @@ def test_panel_graph_equals_eager_and_objective_decreases():
         prev = cur
 
 
+@pytest.mark.parametrize("k", [16, 32, 128])
+def test_panel_interleave_knob_is_bitwise_neutral(k):
+    Ab, B, mu = instance(512, 1024, k, seed=11)
+    pl = PanelLasso(Ab, 2, nrhs=k, device=0)
+    out = []
+    for v in (0, 1, 2):
+        pl.set_tuning("interleave", v)
+        out.append(pl.run(B, mu, 12)["x"])
+    np.testing.assert_array_equal(out[0], out[1])
+    with pytest.raises(Exception):
+        pl.set_tuning("no_such_knob", 1)
+
+
 def test_panel_rejects_bad_shapes():
     with pytest.raises(Exception):
         PanelLasso(np.ones((100, 256)), 1, nrhs=16)
     with pytest.raises(Exception):
-        PanelLasso(np.ones((128, 256)), 1, nrhs=24)
+        PanelLasso(np.ones((256, 256)), 1, nrhs=24)
+    with pytest.raises(Exception):
+        PanelLasso(np.ones((256, 384)), 1, nrhs=16)
