@@ -68,7 +68,8 @@ def parse():
     ap.add_argument("--rhs", type=int, default=1,
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
-    ap.add_argument("--interleave", type=int, default=1, help="panel path: LDS-DMA spread over MFMA groups")
+    ap.add_argument("--interleave", type=int, default=-1,
+                    help="panel path mainloop variant 0/1/2 for both passes (-1: library defaults)")
     return ap.parse_args()
 
 
@@ -240,7 +241,8 @@ def main_panel(args):
     A /= A.norm(dim=1, keepdim=True)
     Xt = torch.randn(n, k, device="cuda", generator=g) * (torch.rand(n, k, device="cuda", generator=g) < 0.4)
     pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks)
-    pl.set_tuning("interleave", args.interleave)
+    if args.interleave >= 0:
+        pl.set_tuning("interleave", args.interleave)
     del A
     Ab = pl.A_bf16.float()
     B = (Ab @ Xt + 0.01 * torch.randn(m, k, device="cuda", generator=g)).double()
@@ -295,7 +297,10 @@ def main_panel(args):
             "bound": "hbm", "kernel": {"pass1_mfma": "k_panel_pass1 (A^T R panel GEMM + shrink)",
                                        "pass2_mfma": "k_panel_pass2 (A D panel GEMM)"}[dom],
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(f"panel_m{m}_n{n}_k{k}", dom), "alg_bytes_per_launch": pb,
+            "traffic": pmc_traffic(f"panel_m{m}_n{n}_k{k}", {"pass1_mfma": "k_panel_pass1",
+                                                              "pass2_mfma": "k_panel_pass2"}[dom]),
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)",
+            "alg_bytes_per_launch": pb,
             "avg_launch_ms": kms[dom],
             "mfma": {"achieved_tflops": tflops, "peak_tflops": MFMA_BF16_DENSE_TFLOPS,
                      "frac": tflops / MFMA_BF16_DENSE_TFLOPS, "flops_per_launch": flops},

@@ -792,7 +792,7 @@ struct bpgl_panel {
     bool timing = false;
     std::vector<hipEvent_t> evs;
     int64_t timed_iters = 0;
-    int interleave = 1;   // LDS-DMA pieces spread over the MFMA groups (tuning knob)
+    int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
 };
 
 namespace {
@@ -848,7 +848,7 @@ int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int 
 }
 template <int NT>
 int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    switch (c->interleave) {
+    switch (c->interleave[which]) {
         case 0: return panel_launch_nt<NT, 0>(c, which, fixed_block, out, mode);
         case 1: return panel_launch_nt<NT, 1>(c, which, fixed_block, out, mode);
         default: return panel_launch_nt<NT, 2>(c, which, fixed_block, out, mode);
@@ -1143,9 +1143,11 @@ int bpgl_panel_kernel_times(bpgl_panel* c, double* avg_ms /* 5 */, int64_t* samp
 
 int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     if (!c || !key) return fail(BPGL_E_ARG, "null argument");
-    if (!strcmp(key, "interleave")) {
+    const bool both = !strcmp(key, "interleave");
+    if (both || !strcmp(key, "interleave1") || !strcmp(key, "interleave2")) {
         if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
-        c->interleave = (int)value;
+        if (both || key[10] == '1') c->interleave[0] = (int)value;
+        if (both || key[10] == '2') c->interleave[1] = (int)value;
     } else {
         return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     }

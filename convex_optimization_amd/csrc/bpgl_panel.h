@@ -94,6 +94,13 @@ struct PanelParams {
 
 constexpr int kLspRows = 1024;    // rows per line-search partial
 
+// Diagnostic builds only (tools/panel_diag.sh; never the shipped library): bit 0 drops the
+// A-side LDS-DMA pieces after the prologue, bit 1 the RHS-side ones -- wrong results, used
+// to split a pass's time into MFMA + LDS and each stream's share.
+#ifndef BPGL_PANEL_DIAG
+#define BPGL_PANEL_DIAG 0
+#endif
+
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
 template <int I, int N, typename F>
@@ -208,6 +215,8 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
     // piece i of stage (so, sa): i < LO -> k-wide piece, else A piece i - LO (this order is what
     // the counted wait below assumes: the youngest LA operations are A pieces)
     auto piece = [&](int i, int so, int bo, int sa, int ba) {
+        if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
+        if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
             panel_op_piece<NT>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave, lane);
         } else if (PASS == 1) {
@@ -303,6 +312,8 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
 #pragma unroll
         for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto piece = [&](int i, int so, int bo, int sa, int ba) {
+        if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
+        if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
             panel_op_piece<NT>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave, lane);
         } else if (PASS == 1) {

@@ -173,7 +173,7 @@ class PanelLasso:
         return self.solver_x_device().to(torch.float64).cpu().numpy().T.copy()   # (n, k)
 
     def set_tuning(self, key, value):
-        """Speed-only knobs (bitwise-identical results): 'interleave' 0/1."""
+        """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave' 0-2."""
         N.check(_lib().bpgl_panel_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_panel_set_tuning")
 
     def set_kernel_timing(self, enable):

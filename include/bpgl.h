@@ -207,10 +207,12 @@ const float* bpgl_panel_x(bpgl_panel* ctx);
 int bpgl_panel_set_kernel_timing(bpgl_panel* ctx, int enable);
 int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce, step, update */,
                             int64_t* samples);
-/* tuning knobs (results are bitwise independent of them): "interleave" 0/1/2 --
- * LDS-DMA pieces issued together after each stage barrier (0), spread over
- * the stage's MFMA groups (1, default), or spread and software-pipelined with
- * fragment reads one MFMA group ahead across the stage barrier (2). */
+/* tuning knobs (results are bitwise independent of them): "interleave1",
+ * "interleave2" (pass 1 / pass 2; "interleave" sets both) 0/1/2 -- LDS-DMA
+ * pieces issued together after each stage barrier (0), spread over the stage's
+ * MFMA groups (1, pass-2 default), or spread and software-pipelined with
+ * fragment reads one MFMA group ahead across the stage barrier (2, pass-1
+ * default). */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
 

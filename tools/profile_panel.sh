@@ -24,4 +24,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -
     $B > $OUT/b_write.json 2> $OUT/write.err
 cd $R
 python3 tools/pmc_summary.py $OUT > $OUT/summary.txt
+python3 tools/pmc_traffic.py $OUT/fetch $OUT/write panel_m8192_n65536_k$K $((2*8192*65536 + 8*$K*(8192+65536)))
 cat $OUT/summary.txt
