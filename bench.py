@@ -274,7 +274,7 @@ def main_panel(args):
     flops = 2 * m * w * k * 2                                    # hi + lo operand halves
     tflops = flops / (kms[dom] * 1e-3) / 1e12
     iters_s = args.steps / el_graph
-    alg_iter = 2 * pb
+    alg_iter = 2 * m * w * 2 + 4 * k * 5 * (w + m)          # SURVEY.md 8d (c5: 2.336e9 B -> 3425 it/s)
     out = {
         "metric": METRIC.replace("fp32", "bf16") + f", {k} right-hand sides",
         "value": iters_s, "unit": f"iters/s ({k} right-hand sides per iteration)",

@@ -552,7 +552,7 @@ int bpgl_comm_init(bpgl_ctx* c, const void* uid, int rank, int nranks) {
     c->nranks = nranks;
     c->p.rank = rank;
     c->p.nranks = nranks;
-    if (nranks > 1) {
+    {   // also for nranks == 1: an explicit request (it runs the sharded code path on one GPU)
         ncclUniqueId id;
         memcpy(&id, uid, 128);
         ncclResult_t nr = ncclCommInitRank(&c->comm, nranks, id, rank);

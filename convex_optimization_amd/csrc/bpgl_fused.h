@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kThreads) void k_iter_b(Params p) {
     if (!arrive_last(p.cnt_chunk + chunk, (unsigned long long)p.nseg)) return;
 
     // ---- row-chunk finisher: s23 rows, pending Ax update, r.s23 / s23.s23 shares
-    const bool multi = p.nranks > 1;
+    const bool multi = p.nranks > 1 || p.has_comm;   // the exchange + k_step_fused finish the step
     double rs = 0.0, ss = 0.0;
     for (long long i = i0 + threadIdx.x; i < i1; i += kThreads) {
         double s = 0.0;

@@ -261,6 +261,30 @@ def test_external_exchange_ranks_match_single(golden, case, world, fused):
     np.testing.assert_allclose(errs[0][:IT], fx["err_iter"][:IT], rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("fused", [0, 1])
+@pytest.mark.parametrize("case", ["c1_b2_p4_f32in", "bound_b4_p2_f32in", "ragged_b3_p2_f32in"])
+def test_single_rank_rccl_path(golden, case, fused):
+    """The RCCL leg (comm init, all-reduce captured in the graph, k_step) with one rank on one GPU:
+    same answers as the reference run and as the communicator-free solver."""
+    from convex_optimization_amd import distributed as D
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    B, IT = int(fx["BLOCK"]), int(fx["ITER_MAX"])
+    eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
+    plain = make_cls("float")(A, B, device=0)
+    plain.set_tuning("fused", fused)
+    ref = plain.run(fx["b"], float(fx["mu"]), IT, err_bound=eb, record=True)
+    gc = make_cls("float")(A, B, device=0, comm=D.RankComm(0, 1))
+    gc.set_tuning("fused", fused)
+    for graph in (True, False):
+        res = gc.run(fx["b"], float(fx["mu"]), IT, err_bound=eb, record=True, use_graph=graph)
+        assert res["t_last"] == int(fx["t_last"]) and res["stopped"] == bool(fx["stopped"])
+        assert rel(res["x"], fx["x"].reshape(-1)) <= 1e-9
+        assert rel(res["x"], ref["x"]) <= 1e-12, rel(res["x"], ref["x"])
+        T = int(fx["t_last"]) + 1
+        np.testing.assert_allclose(res["err_iter"][:T], ref["err_iter"][:T], rtol=1e-12, atol=1e-15)
+
+
 @pytest.mark.parametrize("fused", [1, 0])
 def test_tuning_knobs_do_not_change_results(golden, fused):
     fx = golden("c1_b2_p4_f32in")
