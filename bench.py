@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=20190325)
     ap.add_argument("--fused", type=int, default=0, help="1: two-launch fused iteration; 0 (default): five kernels")
+    ap.add_argument("--comm", action="store_true",
+                    help="attach an RCCL communicator even at N = 1 (runs the sharded/all-reduce leg)")
     ap.add_argument("--rhs", type=int, default=1,
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
@@ -98,11 +100,11 @@ class Ctx:
         return float(t[0])
 
 
-def build_problem(ctx, m, n_total, block, type_name, seed):
+def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False):
     import torch
     from convex_optimization_amd.distributed import RankComm, shard_bounds
     from convex_optimization_amd.parameters import device_instance
-    comm = RankComm(ctx.rank, ctx.world) if ctx.world > 1 else None
+    comm = RankComm(ctx.rank, ctx.world) if (ctx.world > 1 or force_comm) else None
     col_range = None
     if ctx.world > 1:
         bounds = shard_bounds(n_total, block, ctx.rank, ctx.world)
@@ -131,7 +133,7 @@ def timed_window(ctx, gc, steps, graph):
 
 
 def measure(ctx, args, m, n_total):
-    gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed)
+    gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm)
     gc.set_tuning("fused", args.fused)
     # graph replay needs per-kernel events off; timing mode launches eagerly with
     # HIP events around every kernel on the solver stream.
@@ -350,7 +352,7 @@ def main():
                          f"configs[2]-style: m={m} n={n_total} fp32 A, 1 feature block, column-sharded "
                          f"{w} cols/GPU x {G} GPUs, RCCL all-reduce per iteration"),
             "m": m, "n": n_total, "n_local": w, "feature_blocks": args.block, "a_storage": args.type,
-            "accumulate": "fp64", "parallelism": f"column-shard x{G}",
+            "accumulate": "fp64", "parallelism": f"column-shard x{G}", "rccl": bool(G > 1 or args.comm),
             "global_iters_per_s": iters_s_graph,
             "alg_bytes_per_iter_per_gpu": alg_bytes_iter(m, w, sa),
             "hbm_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(m, w, sa),

@@ -758,7 +758,6 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     double sum[kTimedKinds] = {0};
-    const bool multi = c->comm != nullptr || c->external;
     for (int64_t it = 0; it < c->timed_iters; ++it) {
         for (int k = 0; k < kTimedKinds; ++k) {
             if (!c->kind_used[k]) continue;
@@ -894,8 +893,8 @@ int panel_iteration(bpgl_panel* c, int64_t it) {
     LAUNCH_CHECK("k_panel_step");
     panel_ev(c, it, 3, 1);
     panel_ev(c, it, 4, 0);
-    const int64_t n = std::max<int64_t>((int64_t)c->k * c->w, (int64_t)c->k * c->m);
-    hipLaunchKernelGGL(k_panel_update, dim3((unsigned)std::min<int64_t>(cdiv(n, kThreads), 2048)), dim3(kThreads), 0,
+    const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
+    hipLaunchKernelGGL(k_panel_update, dim3((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192)), dim3(kThreads), 0,
                        c->stream, c->p);
     LAUNCH_CHECK("k_panel_update");
     panel_ev(c, it, 4, 1);
@@ -933,6 +932,8 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
         while (w % ((int64_t)kchunks * kPanelK)) --kchunks;
     }
     if (w % ((int64_t)kchunks * kPanelK)) return fail(BPGL_E_ARG, "w must be a multiple of 64 * kchunks");
+    if ((int64_t)nrhs * w >= (1ll << 31) || (int64_t)nrhs * m >= (1ll << 31))
+        return fail(BPGL_E_ARG, "nrhs * block width and nrhs * m must be below 2^31");
     HIP_TRY(hipSetDevice(device));
     bpgl_panel* c = new bpgl_panel();
     c->device = device;

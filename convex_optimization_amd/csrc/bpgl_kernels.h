@@ -223,7 +223,6 @@ __global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __
                                                       double* __restrict__ slab, int fixed_block) {
     constexpr int V = VecT<T>::N;
     constexpr int SEGW = 64 * V * kU;
-    using raw = typename VecT<T>::raw;
     if (fixed_block < 0 && p.st->done) return;
     const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
     const int seg = blockIdx.x % p.nseg;
@@ -428,7 +427,6 @@ __global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __
                                                       double* __restrict__ slab, int fixed_block) {
     constexpr int V = VecT<T>::N;
     constexpr int SEGW = 64 * V * kU;
-    using raw = typename VecT<T>::raw;
     if (fixed_block < 0 && p.st->done) return;
     const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
     const int seg = blockIdx.x % p.nseg;

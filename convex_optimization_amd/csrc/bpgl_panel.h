@@ -531,19 +531,33 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, 
 }
 
 // S = sum over chunks (fp64, fixed order); line-search partials per RHS and
-// 1024-row group (mode 1), or plain output (mode 0, API).  grid = k x (m / 1024)
+// 1024-row group (mode 1), or plain output (mode 0, API).  grid = k x (m / 1024);
+// a thread owns 4 consecutive rows (16-B slab loads).
 __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double* __restrict__ Sout, int mode) {
     const int rhs = blockIdx.x % p.k;
     const int grp = blockIdx.x / p.k;
-    const long long i0 = (long long)grp * kLspRows;
+    const long long i = (long long)grp * kLspRows + 4 * threadIdx.x;
     double rs = 0.0, ss = 0.0;
-    for (long long i = i0 + threadIdx.x; i < i0 + kLspRows && i < p.m; i += kThreads) {
-        double s = 0.0;
-        for (int c = 0; c < p.kchunks; ++c) s += (double)p.Sslab[((long long)c * p.k + rhs) * p.m + i];
-        Sout[(long long)rhs * p.m + i] = s;
+    if (i < p.m) {
+        double s[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int c = 0; c < p.kchunks; ++c) {
+            const float4 v = *reinterpret_cast<const float4*>(p.Sslab + ((long long)c * p.k + rhs) * p.m + i);
+            s[0] += (double)v.x;
+            s[1] += (double)v.y;
+            s[2] += (double)v.z;
+            s[3] += (double)v.w;
+        }
+        double* so = Sout + (long long)rhs * p.m + i;
+        *reinterpret_cast<double2*>(so) = make_double2(s[0], s[1]);
+        *reinterpret_cast<double2*>(so + 2) = make_double2(s[2], s[3]);
         if (mode) {
-            rs = fma(p.R[(long long)rhs * p.m + i], s, rs);
-            ss = fma(s, s, ss);
+            const double* r = p.R + (long long)rhs * p.m + i;
+            const double2 r01 = *reinterpret_cast<const double2*>(r);
+            const double2 r23 = *reinterpret_cast<const double2*>(r + 2);
+            rs = fma(r01.x, s[0], rs); rs = fma(r01.y, s[1], rs);
+            rs = fma(r23.x, s[2], rs); rs = fma(r23.y, s[3], rs);
+            ss = fma(s[0], s[0], ss); ss = fma(s[1], s[1], ss);
+            ss = fma(s[2], s[2], ss); ss = fma(s[3], s[3], ss);
         }
     }
     if (!mode) return;
@@ -597,27 +611,58 @@ __global__ __launch_bounds__(kThreads) void k_panel_step(PanelParams p) {
 }
 
 // x_j += gamma_j D'_j ; Ax_j += gamma_j S_j ; R = sum_b Ax_b - B ; split R.
-// One thread per element of the larger of [k][w] and [k][m]; also bumps t.
+// Work units: u < ux -> 8 consecutive x elements ([k][w], 16-B hi/lo loads); ux <= u <
+// ux + ur -> 4 consecutive residual rows ([k][m]).  Also bumps t.  k*w and k*m < 2^31
+// (checked at create), so the index math is 32-bit.
 __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
     const int mb = (int)p.st->cur_mb;   // p.st->t is advanced by block 0 of this launch
     const long long nx = (long long)p.k * p.w, nr = (long long)p.k * p.m;
-    const long long n = nx > nr ? nx : nr;
-    for (long long e = (long long)blockIdx.x * kThreads + threadIdx.x; e < n; e += (long long)gridDim.x * kThreads) {
-        if (e < nx) {
-            const int rhs = (int)(e / p.w);
-            const double dp = (double)(float)p.Dh[e] + (double)(float)p.Dl[e];
+    const unsigned ux = (unsigned)(nx / 8), ur = (unsigned)(nr / 4);
+    const unsigned nu = ux + ur;
+    const unsigned w8 = (unsigned)(p.w / 8), m4 = (unsigned)(p.m / 4);
+    typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+    for (unsigned u = blockIdx.x * kThreads + threadIdx.x; u < nu; u += gridDim.x * kThreads) {
+        if (u < ux) {
+            const long long e = 8ll * u;
+            const double g = p.gamma[u / w8];
+            const bf16x8v dh = *reinterpret_cast<const bf16x8v*>(p.Dh + e);
+            const bf16x8v dl = *reinterpret_cast<const bf16x8v*>(p.Dl + e);
             float* xp = p.X + (long long)mb * nx + e;
-            *xp = (float)((double)*xp + p.gamma[rhs] * dp);
+            float4 x0 = *reinterpret_cast<const float4*>(xp);
+            float4 x1 = *reinterpret_cast<const float4*>(xp + 4);
+            float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                xs[q] = (float)((double)xs[q] + g * ((double)(float)dh[q] + (double)(float)dl[q]));
+            *reinterpret_cast<float4*>(xp) = make_float4(xs[0], xs[1], xs[2], xs[3]);
+            *reinterpret_cast<float4*>(xp + 4) = make_float4(xs[4], xs[5], xs[6], xs[7]);
         }
-        if (e < nr) {
-            const int rhs = (int)(e / p.m);
+        else {
+            const unsigned v = u - ux;
+            const long long e = 4ll * v;
+            const double g = p.gamma[v / m4];
             double* ap = p.Ax + (long long)mb * nr + e;
-            *ap += p.gamma[rhs] * p.S[e];
-            double acc = p.Ax[e];
-            for (int q = 1; q < p.nblock; ++q) acc += p.Ax[(long long)q * nr + e];
-            const double r = acc - p.B[e];
-            p.R[e] = r;
-            split_bf16(r, p.Rh[e], p.Rl[e]);
+            double a[4], acc[4], r[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = ap[q] + g * p.S[e + q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ap[q] = a[q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = mb == 0 ? a[q] : p.Ax[e + q];
+            for (int b = 1; b < p.nblock; ++b)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] += b == mb ? a[q] : p.Ax[(long long)b * nr + e + q];
+            __bf16 hi[4], lo[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                r[q] = acc[q] - p.B[e + q];
+                split_bf16(r[q], hi[q], lo[q]);
+            }
+            *reinterpret_cast<double2*>(p.R + e) = make_double2(r[0], r[1]);
+            *reinterpret_cast<double2*>(p.R + e + 2) = make_double2(r[2], r[3]);
+            *reinterpret_cast<bf16x4v*>(p.Rh + e) = bf16x4v{hi[0], hi[1], hi[2], hi[3]};
+            *reinterpret_cast<bf16x4v*>(p.Rl + e) = bf16x4v{lo[0], lo[1], lo[2], lo[3]};
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
