@@ -1,0 +1,44 @@
+"""bench.py's algorithmic-byte figures against SURVEY.md 8d (CPU only; no GPU touched)."""
+import importlib.util
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_iteration_bytes_match_survey():
+    b = _bench()
+    c2 = b.alg_bytes_iter(8192, 65536)
+    assert c2 == 2 * 8192 * 65536 * 4 + 8 * (5 * 65536 + 5 * 8192)
+    assert abs(b.HBM_PEAK_GBS * 1e9 / c2 - 1861) < 1.0          # "roofline 1861 it/s"
+    c4 = b.alg_bytes_iter(1048576, 4096)
+    assert abs(c4 - 3.440e10) < 0.001e10 and abs(b.HBM_PEAK_GBS * 1e9 / c4 - 232.5) < 0.5
+
+
+def test_pass_bytes_and_panel_figures():
+    b = _bench()
+    assert b.alg_bytes_colpass(8192, 65536) == 8192 * 65536 * 4 + 8 * 8192 + 8 * 65536
+    assert b.alg_bytes_rowpass(8192, 65536, 2) == 8192 * 65536 * 2 + 8 * 65536 + 8 * 8192
+    # c5 per iteration: 2.336e9 B -> ~3425 it/s; flops 4 m w k = 2.749e11
+    c5 = 2 * 8192 * 65536 * 2 + 4 * 128 * 5 * (65536 + 8192)
+    assert abs(c5 - 2.336e9) < 0.001e9 and abs(8e12 / c5 - 3425) < 1.0
+    assert b.panel_bytes_pass(8192, 65536, 128) == 2 * 8192 * 65536 + 8 * 128 * (8192 + 65536)
+
+
+def test_default_arguments_are_the_headline_config():
+    b = _bench()
+    import sys
+    argv = sys.argv
+    try:
+        sys.argv = ["bench.py"]
+        a = b.parse()
+    finally:
+        sys.argv = argv
+    assert (a.gpus, a.m, a.n_per_gpu, a.block, a.type, a.rhs) == (1, 8192, 65536, 1, "float", 1)
+    assert a.steps > 0 and a.warmup >= 0

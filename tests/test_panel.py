@@ -112,6 +112,41 @@ def test_panel_interleave_knob_is_bitwise_neutral(k):
         pl.set_tuning("no_such_knob", 1)
 
 
+@pytest.mark.parametrize("kchunks", [1, 2, 4, 16])
+def test_panel_split_k_chunks_agree(kchunks):
+    """Pass-2 column chunks only change the fp64 summation order of the fp32 chunk partials."""
+    Ab, B, mu = instance(512, 2048, 32, seed=5)
+    base = PanelLasso(Ab, 1, nrhs=32, device=0).run(B, mu, 30)["x"]
+    pl = PanelLasso(Ab, 1, nrhs=32, device=0, kchunks=kchunks)
+    assert pl.kchunks == kchunks
+    x = pl.run(B, mu, 30)["x"]
+    assert np.linalg.norm(x - base) <= 1e-4 * np.linalg.norm(base)
+
+
+def test_panel_many_blocks_k128_matches_oracle():
+    Ab, B, mu = instance(256, 2048, 128, seed=9)
+    pl = PanelLasso(Ab, 4, nrhs=128, device=0)
+    res = pl.run(B, mu, 40)
+    for j in (0, 63, 127):
+        ref = oracle.run(Ab, B[:, j], mu[j], 4, 40, nthreads=NT)["x"]
+        assert np.linalg.norm(res["x"][:, j] - ref) <= 1e-2 * np.linalg.norm(ref)
+        assert abs(objective(Ab, B[:, j], mu[j], res["x"][:, j]) - objective(Ab, B[:, j], mu[j], ref)) <= \
+            1e-5 * objective(Ab, B[:, j], mu[j], ref)
+
+
+def test_panel_argument_errors():
+    Ab, B, mu = instance(256, 512, 16, seed=2)
+    pl = PanelLasso(Ab, 2, nrhs=16, device=0)
+    with pytest.raises(Exception):
+        pl.mat_tMulMat(np.zeros((256, 16)), 2)
+    with pytest.raises(Exception):
+        pl.matMulMat(np.zeros((256, 16)), -1)
+    with pytest.raises(Exception):
+        pl.solver_step(1)            # no reset yet
+    with pytest.raises(Exception):
+        PanelLasso(Ab, 1, nrhs=16, device=0, kchunks=3)   # 512 columns are not 3 x 64-column chunks
+
+
 def test_panel_rejects_bad_shapes():
     with pytest.raises(Exception):
         PanelLasso(np.ones((100, 256)), 1, nrhs=16)
