@@ -54,7 +54,6 @@ constexpr int kGraphIters = 8;
 constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
-int elem_bytes(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 8 : 2; }
 int64_t up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 }  // namespace
@@ -428,7 +427,7 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
               int64_t scratch_bytes) {
     if (!c) return fail(BPGL_E_ARG, "null context");
     if (!A || !scratch) return fail(BPGL_E_ARG, "A and scratch must be non-null");
-    const int eb = elem_bytes(c->dtype), V = vec_elems(c->dtype);
+    const int V = vec_elems(c->dtype);
     if (((uintptr_t)A) % 16) return fail(BPGL_E_ARG, "A must be 16-byte aligned");
     if (((uintptr_t)scratch) % 256) return fail(BPGL_E_ARG, "scratch must be 256-byte aligned");
     if (lda < c->wp || lda % V) return fail(BPGL_E_ARG, "lda (%lld) must be >= w_pad (%lld) and a multiple of %d",
@@ -436,7 +435,6 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     if (c->nblock > 1 && (block_stride % V || block_stride < c->wp))
         return fail(BPGL_E_ARG, "block_stride (%lld) must be a multiple of %d and >= w_pad",
                     (long long)block_stride, V);
-    (void)eb;
     const Layout L = layout(c);
     if (scratch_bytes < L.total)
         return fail(BPGL_E_SCRATCH, "scratch too small: %lld < %lld", (long long)scratch_bytes, (long long)L.total);
