@@ -1161,3 +1161,10 @@ int bpgl_panel_geometry(const bpgl_panel* c, int32_t* kchunks) {
 }
 
 }  // extern "C"
+
+#if BPGL_STAMP
+// diagnostic builds only: copy the [2][2][16384] block stamps to host memory
+extern "C" int bpgl_diag_stamps(void* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(bpgl::g_stamps), sizeof(bpgl::g_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif

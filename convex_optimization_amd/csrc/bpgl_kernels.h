@@ -218,26 +218,38 @@ __device__ __forceinline__ void colpass_span(const T* __restrict__ Ab, long long
     }
 }
 
+// Diagnostic builds only (tools/stamp_diag.sh, -DBPGL_STAMP=1): per-block start/end times
+// (s_memrealtime, 100 MHz) of the last k_colpass / k_rowpass launch, to measure ramp and tail.
+#ifndef BPGL_STAMP
+#define BPGL_STAMP 0
+#endif
+#if BPGL_STAMP
+__device__ unsigned long long g_stamps[2][2][16384];
+#define BPGL_STAMP_AT(kern, se)                                                                   \
+    do {                                                                                          \
+        if ((se) == 1) __syncthreads();                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < 16384)                                               \
+            g_stamps[kern][se][blockIdx.x] = __builtin_amdgcn_s_memrealtime();                    \
+    } while (0)
+#else
+#define BPGL_STAMP_AT(kern, se) do { } while (0)
+#endif
+
+// one (chunk, seg) tile of the A^T vec pass: rows [chunk R, +R) x the segment's columns,
+// fp64 partials written to slab row `chunk`.  `red` is the block's LDS reduction buffer.
 template <typename T, int MODE, bool NT, int RPT, bool PIPE>
-__global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __restrict__ vec,
-                                                      double* __restrict__ slab, int fixed_block) {
+__device__ __forceinline__ void colpass_tile(const Params& p, const T* __restrict__ Ab, const double* __restrict__ vec,
+                                             double* __restrict__ slab, int seg, int chunk,
+                                             double (&red)[kWaves][kU * VecT<T>::N][64]) {
     constexpr int V = VecT<T>::N;
     constexpr int SEGW = 64 * V * kU;
-    if (fixed_block < 0 && p.st->done) return;
-    const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
-    const int seg = blockIdx.x % p.nseg;
-    const int chunk = blockIdx.x / p.nseg;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
-
     long long col[kU];
-    bool ok[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        long long c = (long long)seg * SEGW + u * 64 * V + lane * V;
-        ok[u] = c < p.wp;
-        col[u] = ok[u] ? c : 0;     // clamped: loads stay in bounds, value masked below
+        const long long c = (long long)seg * SEGW + u * 64 * V + lane * V;
+        col[u] = c < p.wp ? c : 0;  // clamped: loads stay in bounds, the column is dropped below
     }
     double acc[kU][V];
 #pragma unroll
@@ -257,7 +269,6 @@ __global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __
     }
     colpass_span<T, MODE, false, RPT, PIPE>(Ab, p.lda, col, vec, i, i1, i1, acc);
     // cross-wave reduction in a fixed order (wave 0 + 1 + 2 + 3)
-    __shared__ double red[kWaves][kU * V][64];
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -276,6 +287,18 @@ __global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __
 #pragma unroll
         for (int e = 0; e < V; e += 2) *reinterpret_cast<double2*>(dst + e) = make_double2(o[e], o[e + 1]);
     }
+}
+
+template <typename T, int MODE, bool NT, int RPT, bool PIPE>
+__global__ __launch_bounds__(kThreads) void k_colpass(Params p, const double* __restrict__ vec,
+                                                      double* __restrict__ slab, int fixed_block) {
+    if (fixed_block < 0 && p.st->done) return;
+    BPGL_STAMP_AT(0, 0);
+    const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
+    const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
+    __shared__ double red[kWaves][kU * VecT<T>::N][64];
+    colpass_tile<T, MODE, NT, RPT, PIPE>(p, Ab, vec, slab, blockIdx.x % p.nseg, blockIdx.x / p.nseg, red);
+    BPGL_STAMP_AT(0, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -422,19 +445,15 @@ __device__ __forceinline__ void rowpass_group(const T* __restrict__ Ab, long lon
     }
 }
 
+// one (chunk, seg) tile of the A d pass: the segment's d in registers, the chunk's rows,
+// fp64 row partials to out[seg][rows]
 template <typename T, bool NT>
-__global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __restrict__ d,
-                                                      double* __restrict__ slab, int fixed_block) {
+__device__ __forceinline__ void rowpass_tile(const Params& p, const T* __restrict__ Ab, const double* __restrict__ d,
+                                             double* __restrict__ slab, int seg, int chunk) {
     constexpr int V = VecT<T>::N;
     constexpr int SEGW = 64 * V * kU;
-    if (fixed_block < 0 && p.st->done) return;
-    const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
-    const int seg = blockIdx.x % p.nseg;
-    const int chunk = blockIdx.x / p.nseg;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
-
     long long col[kU];
     double dv[kU][V];
 #pragma unroll
@@ -465,6 +484,17 @@ __global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __
         const long long grp = p.reverse_rows ? ngroups - 1 - gi : gi;
         rowpass_group<T, false>(Ab, p.lda, col, dv, i0 + grp * 4 * kWaves + wave, i1, out, lane);
     }
+}
+
+template <typename T, bool NT>
+__global__ __launch_bounds__(kThreads) void k_rowpass(Params p, const double* __restrict__ d,
+                                                      double* __restrict__ slab, int fixed_block) {
+    if (fixed_block < 0 && p.st->done) return;
+    BPGL_STAMP_AT(1, 0);
+    const int mb = fixed_block >= 0 ? fixed_block : cur_block(p);
+    const T* Ab = reinterpret_cast<const T*>(p.A) + (long long)mb * p.block_stride;
+    rowpass_tile<T, NT>(p, Ab, d, slab, blockIdx.x % p.nseg, blockIdx.x / p.nseg);
+    BPGL_STAMP_AT(1, 1);
 }
 
 // ---------------------------------------------------------------------------

@@ -36,8 +36,9 @@ def main():
         os.environ["BPGL_TARGET_BLOCKS"] = str(tb)
         gc, b, mu, _ = device_instance(a.m, a.n, 0.4, a.block, TYPE=a.type, seed=1, device=0)
         geo = gc.geometry()
-        for rev, nt, tail, fu, cm in [(int(r), int(n), int(t), int(f), int(c)) for r in a.reverse.split(",")
-                                      for n in a.nt.split(",") for t in a.tails.split(",") for f in a.fused.split(",")
+        for rev, nt, tail, fu, cm in [(int(r), int(n), int(t), int(f), int(c))
+                                      for r in a.reverse.split(",") for n in a.nt.split(",")
+                                      for t in a.tails.split(",") for f in a.fused.split(",")
                                       for c in a.colmodes.split(",")]:
             gc.set_tuning("fused", fu)
             gc.set_tuning("col_mode", cm)
@@ -59,7 +60,8 @@ def main():
             gc.solver_step(a.steps // 2)
             kt, _ = gc.kernel_times()
             gc.set_kernel_timing(False)
-            rec = dict(target=tb, reverse=rev, nt=nt, tail=tail, fused=fu, col_mode=cm, geometry=geo, iters_per_s=best,
+            rec = dict(target=tb, reverse=rev, nt=nt, tail=tail, fused=fu, col_mode=cm, geometry=geo,
+                       iters_per_s=best,
                        kernel_us={k: round(v * 1e3, 2) for k, v in kt.items()})
             print(json.dumps(rec), flush=True)
             out.append(rec)
