@@ -210,6 +210,31 @@ def vendor_yardstick(gc, reps=20):
             "mtv_GBps": H * K * 4 / t_mtv / 1e6, "mv_GBps": H * K * 4 / t_mv / 1e6}
 
 
+def vendor_iteration_yardstick(gc, b, mu, iters=20):
+    """The whole iteration on rocBLAS GEMVs (yardstick.VendorLasso): fp32
+    GEMVs on the same resident A, fp64 elementwise; iterations/s, eager torch launches."""
+    import torch
+    from convex_optimization_amd.yardstick import VendorLasso
+    A = gc._A_dev
+    if A.dim() != 2 or A.dtype != torch.float32 or gc.Block != 1:
+        return None
+    v = VendorLasso.__new__(VendorLasso)
+    v.Block, v.H, v.W, v.dtype, v.device = 1, A.shape[0], A.shape[1], torch.float32, A.device
+    v.A_b = A.unsqueeze(0)                       # a view: no copy of A
+    v.diag = (A.double() ** 2).sum(dim=0).unsqueeze(0) if A.numel() < (1 << 28) else \
+        torch.stack([(A[:, j:j + 4096].double() ** 2).sum(dim=0) for j in range(0, A.shape[1], 4096)]).reshape(1, -1)
+    v.rec = 1.0 / v.diag
+    v.reset(b, mu)
+    v.step(3)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    v.step(iters)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"what": "yardstick.VendorLasso: the iteration with torch.mv (rocBLAS/hipBLASLt) fp32 GEMVs + torch "
+                    "elementwise, fp64 vectors, eager launches", "iters_per_s": iters / el, "iters": iters}
+
+
 def pmc_traffic(workload_key, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
@@ -385,6 +410,7 @@ def main():
         res = strong
     if G == 1 and args.type == "float":
         out["config"]["vendor_gemv_yardstick"] = vendor_yardstick(res["gc"])
+        out["config"]["vendor_iteration_yardstick"] = vendor_iteration_yardstick(res["gc"], res["b"], res["mu"])
     if G == 1 and ctx.rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds)
     if ctx.rank == 0:

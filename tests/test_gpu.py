@@ -285,6 +285,19 @@ def test_single_rank_rccl_path(golden, case, fused):
         np.testing.assert_allclose(res["err_iter"][:T], ref["err_iter"][:T], rtol=1e-12, atol=1e-15)
 
 
+@pytest.mark.parametrize("case", ["c1_b1_p1_f64", "c1_b2_p4_f64", "ragged_b3_p2_f32in"])
+def test_vendor_yardstick_reproduces_reference(golden, case):
+    """The rocBLAS-GEMV yardstick (yardstick.VendorLasso, fp64) runs the same iteration."""
+    from convex_optimization_amd.yardstick import VendorLasso
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    B, IT = int(fx["BLOCK"]), int(fx["ITER_MAX"])
+    v = VendorLasso(A, B, dtype=torch.float64, device=0)
+    v.reset(fx["b"], float(fx["mu"]))
+    v.step(IT)
+    assert rel(v.solution(), fx["x"].reshape(-1)) <= 1e-9
+
+
 @pytest.mark.parametrize("fused", [1, 0])
 def test_tuning_knobs_do_not_change_results(golden, fused):
     fx = golden("c1_b2_p4_f32in")
