@@ -104,8 +104,10 @@ void geometry(bpgl_ctx* c) {
     c->segw = 64 * V * kU;
     c->wp = up(c->w, V);
     c->nseg = (int)cdiv(c->wp, c->segw);
-    // ~8 blocks per CU on 256 CUs, rows per chunk a multiple of 16 (4 waves x 4 rows)
-    int64_t target = 1024;
+    // tiles per launch (rows per chunk a multiple of 16 = 4 waves x 4 rows): one resident wave
+    // of 1024 blocks for fp32; fp64 and bf16 A measured ~3 % faster at 512
+    // (profiles/r01/sweeps: tile-count sweeps per storage type)
+    int64_t target = c->dtype == BPGL_F32 ? 1024 : 512;
     if (const char* e = getenv("BPGL_TARGET_BLOCKS")) target = std::max<int64_t>(1, atoll(e));
     int64_t nchunk = std::max<int64_t>(1, cdiv(target, c->nseg));
     nchunk = std::min<int64_t>(nchunk, cdiv(c->m, 16));
