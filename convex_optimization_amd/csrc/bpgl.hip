@@ -18,13 +18,13 @@
 #include <vector>
 
 #include "../../include/bpgl.h"
+#include "bpgl_host.h"
 #include "bpgl_kernels.h"
 #include "bpgl_fused.h"
-#include "bpgl_panel.h"
 
 using namespace bpgl;
 
-namespace {
+namespace bpgl_host {
 thread_local std::string g_err;
 
 int fail(int code, const char* fmt, ...) {
@@ -36,26 +36,14 @@ int fail(int code, const char* fmt, ...) {
     g_err = buf;
     return code;
 }
+}  // namespace bpgl_host
+using namespace bpgl_host;
 
-#define HIP_TRY(expr)                                                                        \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess) return fail(BPGL_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-    } while (0)
-
-#define LAUNCH_CHECK(what)                                                                   \
-    do {                                                                                     \
-        hipError_t e_ = hipGetLastError();                                                   \
-        if (e_ != hipSuccess) return fail(BPGL_E_HIP, "launch %s: %s", what, hipGetErrorString(e_)); \
-    } while (0)
-
+namespace {
 constexpr int kTimedKinds = 7;
-constexpr int kGraphIters = 8;
 constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
-int64_t up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
-int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 }  // namespace
 
 struct bpgl_ctx {
@@ -116,15 +104,6 @@ void geometry(bpgl_ctx* c) {
     c->nchunk = (int)cdiv(c->m, R);
     c->nparts = (int)cdiv(c->wp, kColsPerShrink);
 }
-
-struct Carve {
-    int64_t off = 0;
-    int64_t take(int64_t bytes) {
-        int64_t o = off;
-        off = up(off + bytes, 256);
-        return o;
-    }
-};
 
 // scratch layout (offsets in bytes)
 struct Layout {
@@ -359,7 +338,7 @@ int enqueue_iteration(bpgl_ctx* c, int64_t it) {
 
 extern "C" {
 
-const char* bpgl_last_error(void) { return g_err.c_str(); }
+const char* bpgl_last_error(void) { return bpgl_host::g_err.c_str(); }
 int bpgl_version(void) { return 100; }
 
 int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_local, int32_t nblock,
@@ -772,393 +751,6 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     if (samples) *samples = c->timed_iters;
     c->timed_iters = 0;
     for (int k = 0; k < kTimedKinds; ++k) c->kind_used[k] = false;
-    return 0;
-}
-
-}  // extern "C"
-
-// ===========================================================================
-// panel path (k right-hand sides, bf16 A, MFMA): BASELINE configs[4]
-// ===========================================================================
-struct bpgl_panel {
-    int device = 0;
-    int64_t m = 0, n = 0, w = 0;
-    int32_t nblock = 1, k = 0, kchunks = 1;
-    hipStream_t stream = nullptr;
-    bool own_stream = false, bound = false, have_diag = false, solver = false;
-    PanelParams p{};
-    hipGraphExec_t gexec = nullptr;
-    bool timing = false;
-    std::vector<hipEvent_t> evs;
-    int64_t timed_iters = 0;
-    int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
-};
-
-namespace {
-constexpr int kPanelKinds = 5;   // pass1, pass2, reduce, step, update
-
-struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, total;
-};
-PanelLayout panel_layout(const bpgl_panel* c) {
-    Carve k;
-    PanelLayout L;
-    const int64_t km = (int64_t)c->k * c->m, kw = (int64_t)c->k * c->w;
-    L.st = k.take(sizeof(PanelState));
-    L.Rh = k.take(2 * km);
-    L.Rl = k.take(2 * km);
-    L.Dh = k.take(2 * kw);
-    L.Dl = k.take(2 * kw);
-    L.X = k.take(4 * kw * c->nblock);
-    L.Ax = k.take(8 * km * c->nblock);
-    L.B = k.take(8 * km);
-    L.R = k.take(8 * km);
-    L.diag = k.take(8 * c->n);
-    L.rec = k.take(8 * c->n);
-    L.Sslab = k.take(4 * km * c->kchunks);
-    L.S = k.take(8 * km);
-    L.norms = k.take(8 * 4 * (c->w / kPanelRows) * c->k);
-    L.lsp = k.take(8 * 2 * cdiv(c->m, kLspRows) * c->k);
-    L.mu = k.take(8 * c->k);
-    L.gamma = k.take(8 * c->k);
-    L.err_rhs = k.take(8 * c->k);
-    L.total = k.off;
-    return L;
-}
-
-template <int NT, int ILV>
-int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    const dim3 b(PanelGeo<NT>::T);
-    switch (which) {
-        case 0:
-            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV>), dim3((unsigned)(c->w / kPanelRows)), b, 0,
-                                         c->stream, c->p, fixed_block, out);
-            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV>), dim3((unsigned)(c->w / kPanelRows)), b, 0,
-                                    c->stream, c->p, fixed_block, out);
-            LAUNCH_CHECK("k_panel_pass1");
-            break;
-        case 1:
-            hipLaunchKernelGGL((k_panel_pass2<NT, ILV>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)), b, 0,
-                               c->stream, c->p, fixed_block);
-            LAUNCH_CHECK("k_panel_pass2");
-            break;
-    }
-    return 0;
-}
-template <int NT>
-int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    switch (c->interleave[which]) {
-        case 0: return panel_launch_nt<NT, 0>(c, which, fixed_block, out, mode);
-        case 1: return panel_launch_nt<NT, 1>(c, which, fixed_block, out, mode);
-        default: return panel_launch_nt<NT, 2>(c, which, fixed_block, out, mode);
-    }
-}
-int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    switch (c->k) {
-        case 16: return panel_launch_ilv<1>(c, which, fixed_block, out, mode);
-        case 32: return panel_launch_ilv<2>(c, which, fixed_block, out, mode);
-        case 64: return panel_launch_ilv<4>(c, which, fixed_block, out, mode);
-        default: return panel_launch_ilv<8>(c, which, fixed_block, out, mode);
-    }
-}
-int panel_reduce(bpgl_panel* c, double* out, int mode) {
-    hipLaunchKernelGGL(k_panel_reduce, dim3((unsigned)(c->k * cdiv(c->m, kLspRows))), dim3(kThreads), 0, c->stream,
-                       c->p, out, mode);
-    LAUNCH_CHECK("k_panel_reduce");
-    return 0;
-}
-void panel_ev(bpgl_panel* c, int64_t it, int kind, int end) {
-    if (!c->timing) return;
-    const size_t idx = 2 * ((size_t)it * kPanelKinds + kind) + end;
-    while (c->evs.size() <= idx) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return;
-        c->evs.push_back(e);
-    }
-    hipEventRecord(c->evs[idx], c->stream);
-}
-int panel_iteration(bpgl_panel* c, int64_t it) {
-    int rc;
-    panel_ev(c, it, 0, 0);
-    if ((rc = panel_launch(c, 0, -1, nullptr, 1))) return rc;
-    panel_ev(c, it, 0, 1);
-    panel_ev(c, it, 1, 0);
-    if ((rc = panel_launch(c, 1, -1, nullptr, 1))) return rc;
-    panel_ev(c, it, 1, 1);
-    panel_ev(c, it, 2, 0);
-    if ((rc = panel_reduce(c, c->p.S, 1))) return rc;
-    panel_ev(c, it, 2, 1);
-    panel_ev(c, it, 3, 0);
-    hipLaunchKernelGGL(k_panel_step, dim3((unsigned)c->k), dim3(kThreads), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_panel_step");
-    panel_ev(c, it, 3, 1);
-    panel_ev(c, it, 4, 0);
-    const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
-    hipLaunchKernelGGL(k_panel_update, dim3((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192)), dim3(kThreads), 0,
-                       c->stream, c->p);
-    LAUNCH_CHECK("k_panel_update");
-    panel_ev(c, it, 4, 1);
-    return 0;
-}
-int panel_split(bpgl_panel* c, const double* src, int64_t n, __bf16* hi, __bf16* lo, double sign, double* copy) {
-    hipLaunchKernelGGL(k_panel_split, dim3((unsigned)std::min<int64_t>(cdiv(n, kThreads), 2048)), dim3(kThreads), 0,
-                       c->stream, src, n, hi, lo, sign, copy);
-    LAUNCH_CHECK("k_panel_split");
-    return 0;
-}
-int panel_ready(const bpgl_panel* c) {
-    if (!c) return fail(BPGL_E_ARG, "null panel context");
-    if (!c->bound) return fail(BPGL_E_STATE, "bpgl_panel_bind has not been called");
-    return 0;
-}
-}  // namespace
-
-extern "C" {
-
-int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_t nblock, int32_t nrhs,
-                      int32_t kchunks, void* hip_stream) {
-    if (!out) return fail(BPGL_E_ARG, "out is null");
-    *out = nullptr;
-    if (nrhs != 16 && nrhs != 32 && nrhs != 64 && nrhs != 128)
-        return fail(BPGL_E_ARG, "nrhs must be 16, 32, 64 or 128 (got %d)", nrhs);
-    if (nblock <= 0 || n % nblock) return fail(BPGL_E_ARG, "n must be divisible by nblock");
-    const int64_t w = n / nblock;
-    if (m <= 0 || m % kPanelRows) return fail(BPGL_E_ARG, "m (%lld) must be a positive multiple of %d", (long long)m,
-                                              kPanelRows);
-    if (w <= 0 || w % kPanelRows) return fail(BPGL_E_ARG, "block width (%lld) must be a positive multiple of %d",
-                                              (long long)w, kPanelRows);
-    if (kchunks <= 0) {   // one pass-2 tile per CU (256), chunk width a multiple of the 64-deep stage
-        kchunks = (int32_t)std::max<int64_t>(1, std::min<int64_t>(w / kPanelK, 256 / (m / kPanelRows)));
-        while (w % ((int64_t)kchunks * kPanelK)) --kchunks;
-    }
-    if (w % ((int64_t)kchunks * kPanelK)) return fail(BPGL_E_ARG, "w must be a multiple of 64 * kchunks");
-    if ((int64_t)nrhs * w >= (1ll << 31) || (int64_t)nrhs * m >= (1ll << 31))
-        return fail(BPGL_E_ARG, "nrhs * block width and nrhs * m must be below 2^31");
-    HIP_TRY(hipSetDevice(device));
-    bpgl_panel* c = new bpgl_panel();
-    c->device = device;
-    c->m = m;
-    c->n = n;
-    c->w = w;
-    c->nblock = nblock;
-    c->k = nrhs;
-    c->kchunks = kchunks;
-    if (hip_stream) {
-        c->stream = (hipStream_t)hip_stream;
-    } else {
-        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-            delete c;
-            return fail(BPGL_E_HIP, "hipStreamCreate failed");
-        }
-        c->own_stream = true;
-    }
-    *out = c;
-    return 0;
-}
-
-void bpgl_panel_destroy(bpgl_panel* c) {
-    if (!c) return;
-    hipSetDevice(c->device);
-    if (c->gexec) hipGraphExecDestroy(c->gexec);
-    for (auto e : c->evs) hipEventDestroy(e);
-    if (c->own_stream) hipStreamDestroy(c->stream);
-    delete c;
-}
-
-int64_t bpgl_panel_scratch_bytes(const bpgl_panel* c) { return c ? panel_layout(c).total : -1; }
-
-int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, int64_t scratch_bytes) {
-    if (!c) return fail(BPGL_E_ARG, "null panel context");
-    if (!A || !scratch) return fail(BPGL_E_ARG, "A and scratch must be non-null");
-    if (((uintptr_t)A) % 16) return fail(BPGL_E_ARG, "A must be 16-byte aligned");
-    if (((uintptr_t)scratch) % 256) return fail(BPGL_E_ARG, "scratch must be 256-byte aligned");
-    if (lda < c->n || lda % 8) return fail(BPGL_E_ARG, "lda must be >= n and a multiple of 8");
-    const PanelLayout L = panel_layout(c);
-    if (scratch_bytes < L.total) return fail(BPGL_E_SCRATCH, "scratch too small: %lld < %lld",
-                                             (long long)scratch_bytes, (long long)L.total);
-    char* s = (char*)scratch;
-    PanelParams& p = c->p;
-    p = PanelParams{};
-    p.A = (const __bf16*)A;
-    p.lda = lda;
-    p.m = c->m;
-    p.w = c->w;
-    p.nblock = c->nblock;
-    p.k = c->k;
-    p.kchunks = c->kchunks;
-    p.st = (PanelState*)(s + L.st);
-    p.Rh = (__bf16*)(s + L.Rh);
-    p.Rl = (__bf16*)(s + L.Rl);
-    p.Dh = (__bf16*)(s + L.Dh);
-    p.Dl = (__bf16*)(s + L.Dl);
-    p.X = (float*)(s + L.X);
-    p.Ax = (double*)(s + L.Ax);
-    p.B = (const double*)(s + L.B);
-    p.R = (double*)(s + L.R);
-    p.diag = (const double*)(s + L.diag);
-    p.rec = (const double*)(s + L.rec);
-    p.Sslab = (float*)(s + L.Sslab);
-    p.S = (double*)(s + L.S);
-    p.norms = (double*)(s + L.norms);
-    p.lsp = (double*)(s + L.lsp);
-    p.mu = (const double*)(s + L.mu);
-    p.gamma = (double*)(s + L.gamma);
-    p.err_rhs = (double*)(s + L.err_rhs);
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
-    c->bound = true;
-    c->have_diag = false;
-    c->solver = false;
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-    return 0;
-}
-
-int bpgl_panel_diag(bpgl_panel* c, double* out) {
-    int rc;
-    if ((rc = panel_ready(c))) return rc;
-    HIP_TRY(hipSetDevice(c->device));
-    hipLaunchKernelGGL(k_panel_diag, dim3((unsigned)cdiv(c->n, 512)), dim3(kThreads), 0, c->stream, c->p,
-                       const_cast<double*>(c->p.diag), const_cast<double*>(c->p.rec));
-    LAUNCH_CHECK("k_panel_diag");
-    if (out) HIP_TRY(hipMemcpyAsync(out, c->p.diag, 8 * c->n, hipMemcpyDeviceToDevice, c->stream));
-    c->have_diag = true;
-    return 0;
-}
-
-int bpgl_panel_mtm(bpgl_panel* c, int32_t block, const double* R, double* G) {
-    int rc;
-    if ((rc = panel_ready(c))) return rc;
-    if (block < 0 || block >= c->nblock) return fail(BPGL_E_ARG, "block out of range");
-    if (!R || !G) return fail(BPGL_E_ARG, "null operand");
-    HIP_TRY(hipSetDevice(c->device));
-    if ((rc = panel_split(c, R, (int64_t)c->k * c->m, c->p.Rh, c->p.Rl, 1.0, nullptr))) return rc;
-    c->solver = false;   // Rh/Rl now hold the caller's operand
-    return panel_launch(c, 0, block, G, 0);
-}
-
-int bpgl_panel_mm(bpgl_panel* c, int32_t block, const double* D, double* S) {
-    int rc;
-    if ((rc = panel_ready(c))) return rc;
-    if (block < 0 || block >= c->nblock) return fail(BPGL_E_ARG, "block out of range");
-    if (!D || !S) return fail(BPGL_E_ARG, "null operand");
-    HIP_TRY(hipSetDevice(c->device));
-    if ((rc = panel_split(c, D, (int64_t)c->k * c->w, c->p.Dh, c->p.Dl, 1.0, nullptr))) return rc;
-    c->solver = false;
-    if ((rc = panel_launch(c, 1, block, nullptr, 0))) return rc;
-    return panel_reduce(c, S, 0);
-}
-
-int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* err_iter, int64_t record_len,
-                     int use_graph) {
-    int rc;
-    if ((rc = panel_ready(c))) return rc;
-    if (!c->have_diag) return fail(BPGL_E_STATE, "bpgl_panel_diag must run before the solver");
-    if (!B || !mu) return fail(BPGL_E_ARG, "B and mu must be non-null");
-    HIP_TRY(hipSetDevice(c->device));
-    PanelParams& p = c->p;
-    const int64_t km = (int64_t)c->k * c->m;
-    HIP_TRY(hipMemcpyAsync(const_cast<double*>(p.B), B, 8 * km, hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(const_cast<double*>(p.mu), mu, 8 * c->k, hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(p.X, 0, 4 * (int64_t)c->k * c->w * c->nblock, c->stream));
-    HIP_TRY(hipMemsetAsync(p.Ax, 0, 8 * km * c->nblock, c->stream));
-    // x = 0 => Ax = 0, R = -B
-    if ((rc = panel_split(c, p.B, km, p.Rh, p.Rl, -1.0, p.R))) return rc;
-    p.err_iter = err_iter;
-    p.rec_len = err_iter ? record_len : 0;
-    hipLaunchKernelGGL(k_panel_reset_state, dim3(1), dim3(64), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_panel_reset_state");
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-    if (use_graph) {
-        hipGraph_t graph = nullptr;
-        const bool was = c->timing;
-        c->timing = false;
-        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        rc = 0;
-        for (int k = 0; k < kGraphIters && !rc; ++k) rc = panel_iteration(c, 0);
-        hipError_t ec = hipStreamEndCapture(c->stream, &graph);
-        c->timing = was;
-        if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
-        if (ec != hipSuccess) return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
-        hipError_t ei = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
-        if (ei != hipSuccess) return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
-    }
-    c->solver = true;
-    c->timed_iters = 0;
-    return 0;
-}
-
-int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
-    int rc;
-    if ((rc = panel_ready(c))) return rc;
-    if (!c->solver) return fail(BPGL_E_STATE, "bpgl_panel_reset has not been called");
-    HIP_TRY(hipSetDevice(c->device));
-    int64_t i = 0;
-    if (!c->timing && c->gexec)
-        for (; i + kGraphIters <= n_iter; i += kGraphIters) HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
-    for (; i < n_iter; ++i) {
-        if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
-        if (c->timing) c->timed_iters++;
-    }
-    return 0;
-}
-
-int bpgl_panel_status(bpgl_panel* c, int64_t* iters, double* last_err) {
-    int rc;
-    if ((rc = panel_ready(c))) return rc;
-    HIP_TRY(hipSetDevice(c->device));
-    PanelState st;
-    HIP_TRY(hipMemcpyAsync(&st, c->p.st, sizeof st, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (iters) *iters = st.iters;
-    if (last_err) *last_err = st.last_err;
-    return 0;
-}
-
-const float* bpgl_panel_x(bpgl_panel* c) { return c ? c->p.X : nullptr; }
-
-int bpgl_panel_set_kernel_timing(bpgl_panel* c, int enable) {
-    if (!c) return fail(BPGL_E_ARG, "null panel context");
-    c->timing = enable != 0;
-    c->timed_iters = 0;
-    return 0;
-}
-
-int bpgl_panel_kernel_times(bpgl_panel* c, double* avg_ms /* 5 */, int64_t* samples) {
-    if (!c || !avg_ms) return fail(BPGL_E_ARG, "null argument");
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    double sum[kPanelKinds] = {0};
-    for (int64_t it = 0; it < c->timed_iters; ++it)
-        for (int k = 0; k < kPanelKinds; ++k) {
-            const size_t i0 = 2 * ((size_t)it * kPanelKinds + k);
-            float ms = 0.f;
-            HIP_TRY(hipEventElapsedTime(&ms, c->evs[i0], c->evs[i0 + 1]));
-            sum[k] += ms;
-        }
-    for (int k = 0; k < kPanelKinds; ++k) avg_ms[k] = c->timed_iters ? sum[k] / c->timed_iters : 0.0;
-    if (samples) *samples = c->timed_iters;
-    c->timed_iters = 0;
-    return 0;
-}
-
-int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
-    if (!c || !key) return fail(BPGL_E_ARG, "null argument");
-    const bool both = !strcmp(key, "interleave");
-    if (both || !strcmp(key, "interleave1") || !strcmp(key, "interleave2")) {
-        if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
-        if (both || key[10] == '1') c->interleave[0] = (int)value;
-        if (both || key[10] == '2') c->interleave[1] = (int)value;
-    } else {
-        return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
-    }
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-    return 0;
-}
-
-int bpgl_panel_geometry(const bpgl_panel* c, int32_t* kchunks) {
-    if (!c) return fail(BPGL_E_ARG, "null panel context");
-    if (kchunks) *kchunks = c->kchunks;
     return 0;
 }
 

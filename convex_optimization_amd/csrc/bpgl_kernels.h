@@ -1,4 +1,5 @@
-// bpgl device kernels (gfx950 / CDNA4).  Included by bpgl.hip only.
+// bpgl device kernels (gfx950 / CDNA4) of the single-right-hand-side path.
+// Included by bpgl.hip only (non-template kernels are defined here).
 //
 // Hot path of one block update (reference lasso.py:102-157):
 //   k_colpass   partial  g = A_b^T r  over a (row chunk x column segment) tile,
@@ -20,10 +21,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bpgl_device.h"
+
 namespace bpgl {
 
-constexpr int kThreads = 256;   // 4 waves of 64
-constexpr int kWaves = 4;
 constexpr int kU = 4;           // 16-byte loads per lane per row segment (= kWaves)
 
 struct DevState {
@@ -128,16 +129,6 @@ __device__ __forceinline__ int cur_block(const Params& p) {
     return (int)(t % p.nblock);
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { double u = __shfl_xor(v, o); v = (u > v || u != u) ? u : v; }
-    return v;
-}
 
 // ---------------------------------------------------------------------------
 // colpass: slab[chunk][col] = sum_{i in chunk} A_b[i][col] * vec[i]   (MODE 0)
@@ -318,15 +309,6 @@ __global__ __launch_bounds__(kThreads) void k_colreduce(const double* __restrict
 // ---------------------------------------------------------------------------
 // shrink (s14/s15 + error criterion), one thread per column of block mb
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double soft_thr(double t, double tau) {   // cpu_calculation.py:5-6
-    const double mag = fabs(t) - tau;
-    const double sg = t > 0.0 ? 1.0 : (t < 0.0 ? -1.0 : 0.0);
-    return sg * (mag > 0.0 ? mag : 0.0);
-}
-__device__ __forceinline__ double proj(double v, double lo, double hi) {  // cpu_calculation.py:10-11
-    const double a = v < hi ? v : hi;
-    return a > lo ? a : lo;
-}
 
 // block = 64 columns x 4 waves: wave q sums row chunks q, q+4, ... of the slab
 // for its 64 columns, the 4 wave sums are added in a fixed order, wave 0 runs

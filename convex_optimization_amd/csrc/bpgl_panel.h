@@ -28,7 +28,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "bpgl_kernels.h"
+#include "bpgl_device.h"
 
 namespace bpgl {
 

@@ -6,6 +6,6 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p $R/build_diag
 for d in 1 2 3; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DBPGL_PANEL_DIAG=$d \
-    -I$R/include $R/convex_optimization_amd/csrc/bpgl.hip -o $R/build_diag/libbpgl_d$d.so -lrccl &
+    -I$R/include $R/convex_optimization_amd/csrc/bpgl.hip $R/convex_optimization_amd/csrc/bpgl_panel_abi.hip -o $R/build_diag/libbpgl_d$d.so -lrccl &
 done
 wait

@@ -5,4 +5,4 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p $R/build_diag
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DBPGL_STAMP=1 -I$R/include \
-    $R/convex_optimization_amd/csrc/bpgl.hip -o $R/build_diag/libbpgl_stamp.so -lrccl
+    $R/convex_optimization_amd/csrc/bpgl.hip $R/convex_optimization_amd/csrc/bpgl_panel_abi.hip -o $R/build_diag/libbpgl_stamp.so -lrccl
