@@ -53,6 +53,9 @@ def alg_bytes_rowpass(m, w, sa=4):
 
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
+                    help="BASELINE.json configs[K]: 1 = 8192x65536 fp32 (default), 2 = its column-sharded "
+                         "multi-GPU form, 3 = 1048576x4096 fp32, 4 = k=128 right-hand sides on bf16 A")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
@@ -72,7 +75,13 @@ def parse():
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
     ap.add_argument("--interleave", type=int, default=-1,
                     help="panel path mainloop variant 0/1/2 for both passes (-1: library defaults)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config == 3:
+        a.m, a.n_per_gpu = 1048576, 4096
+        a.steps, a.warmup = min(a.steps, 30), min(a.warmup, 5)
+    elif a.config == 4:
+        a.rhs = 128
+    return a
 
 
 class Ctx:

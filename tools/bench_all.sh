@@ -1,0 +1,12 @@
+#!/bin/bash
+# Every single-GPU BASELINE config through bench.py (one JSON line each) into
+# gpurun_out/bench_all/; run on the GPU box from the repo root.
+set -e
+OUT=gpurun_out/bench_all
+mkdir -p $OUT
+timeout -k 10 300 python bench.py --config 1 > $OUT/config1.json 2> $OUT/config1.err
+timeout -k 10 300 python bench.py --config 3 --no-cpu > $OUT/config3.json 2> $OUT/config3.err
+timeout -k 10 300 python bench.py --config 4 --no-cpu --steps 100 > $OUT/config4.json 2> $OUT/config4.err
+timeout -k 10 300 python bench.py --config 1 --type double --no-cpu --steps 100 > $OUT/config1_f64.json 2> $OUT/config1_f64.err
+timeout -k 10 300 python bench.py --config 1 --type bf16 --no-cpu > $OUT/config1_bf16.json 2> $OUT/config1_bf16.err
+timeout -k 10 300 python bench.py --config 1 --block 4 --no-cpu > $OUT/config1_b4.json 2> $OUT/config1_b4.err
