@@ -38,6 +38,17 @@ def alg_bytes_iter(m, w, sa=4, sv=8, k=1):
     return 2 * m * w * sa + sv * k * (5 * w + 5 * m)
 
 
+def alg_bytes_iter_onepass(m, w, sa=4, sv=8):
+    """The one-pass iteration (bpgl_onepass.h): the same vector I/O, A read once."""
+    return m * w * sa + sv * (5 * w + 5 * m)
+
+
+def alg_bytes_onepass(m, w, sa=4):
+    """k_onepass per launch: read A_b (m x w) and D (w fp64), write s23 (m fp64) and
+    U = A^T s23 (w fp64) once."""
+    return m * w * sa + 8 * m + 16 * w
+
+
 def alg_bytes_colpass(m, w, sa=4):
     """A^T s11 pass per launch (k_iter_a / k_colpass): read A_b (m x w) and s11
     (m fp64), produce g once (w fp64).  The shrink's x/D vector I/O is left out
@@ -68,6 +79,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=20190325)
     ap.add_argument("--fused", type=int, default=0, help="1: two-launch fused iteration; 0 (default): five kernels")
+    ap.add_argument("--onepass", type=int, default=-1, choices=[-1, 0, 1],
+                    help="one pass over A per iteration: -1 (default) when eligible (1 block, 1 rank), 0 off, 1 required")
     ap.add_argument("--comm", action="store_true",
                     help="attach an RCCL communicator even at N = 1 (runs the sharded/all-reduce leg)")
     ap.add_argument("--rhs", type=int, default=1,
@@ -144,6 +157,7 @@ def timed_window(ctx, gc, steps, graph):
 def measure(ctx, args, m, n_total):
     gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm)
     gc.set_tuning("fused", args.fused)
+    gc.set_tuning("onepass", args.onepass)
     # graph replay needs per-kernel events off; timing mode launches eagerly with
     # HIP events around every kernel on the solver stream.
     gc.solver_reset(b, mu, use_graph=True)
@@ -359,13 +373,19 @@ def main():
     iters_s_graph = args.steps / res["el_graph"]
     iters_s_ev = args.steps / res["el_events"]
     kms = res["kernel_ms"]
-    dom = max(("colpass", "rowpass"), key=lambda k: kms[k])
     sa = {"float": 4, "double": 8, "bf16": 2}[args.type]
-    dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(m, w, sa)
+    onepass = kms.get("onepass", 0.0) > 0
+    if onepass:
+        dom, dom_bytes, kname = "onepass", alg_bytes_onepass(m, w, sa), "k_onepass"
+        it_bytes = alg_bytes_iter_onepass(m, w, sa)
+    else:
+        dom = max(("colpass", "rowpass"), key=lambda k: kms[k])
+        dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(m, w, sa)
+        kname = {("colpass", 1): "k_iter_a", ("rowpass", 1): "k_iter_b",
+                 ("colpass", 0): "k_colpass", ("rowpass", 0): "k_rowpass"}[(dom, int(args.fused))]
+        it_bytes = alg_bytes_iter(m, w, sa)
     achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
     workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}"
-    kname = {("colpass", 1): "k_iter_a", ("rowpass", 1): "k_iter_b",
-             ("colpass", 0): "k_colpass", ("rowpass", 0): "k_rowpass"}[(dom, int(args.fused))]
     traffic = pmc_traffic(workload_key, kname)
     out = {
         "metric": METRIC,
@@ -388,9 +408,14 @@ def main():
             "m": m, "n": n_total, "n_local": w, "feature_blocks": args.block, "a_storage": args.type,
             "accumulate": "fp64", "parallelism": f"column-shard x{G}", "rccl": bool(G > 1 or args.comm),
             "global_iters_per_s": iters_s_graph,
-            "alg_bytes_per_iter_per_gpu": alg_bytes_iter(m, w, sa),
-            "hbm_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(m, w, sa),
-            "iter_roofline_frac": iters_s_graph * alg_bytes_iter(m, w, sa) / (HBM_PEAK_GBS * 1e9),
+            "iteration": ("one pass over A (k_onepass: s23 = A D and U = A^T s23 together; g += gamma U, "
+                          "exact g = A^T r every 64 iterations)" if onepass else
+                          "two passes over A (A^T r, then A D)"),
+            "alg_bytes_per_iter_per_gpu": it_bytes,
+            "hbm_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / it_bytes,
+            "iter_roofline_frac": iters_s_graph * it_bytes / (HBM_PEAK_GBS * 1e9),
+            "two_pass_alg_bytes_per_iter_per_gpu": alg_bytes_iter(m, w, sa),
+            "two_pass_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(m, w, sa),
             "launch_mode": "hipGraph replay of one iteration (value); eager + HIP events (kernel times)", "fused": args.fused,
             "iters_per_s_eager_with_events": iters_s_ev,
             "kernel_avg_ms": kms,
@@ -399,7 +424,8 @@ def main():
             "bound": "hbm",
             "kernel": kname + ({"k_iter_a": " (A^T s11 pass + segment-finisher shrink)",
                                 "k_iter_b": " (A D pass + row-chunk finishers + line search)",
-                                "k_colpass": " (A^T s11 pass)", "k_rowpass": " (A D pass)"}[kname]),
+                                "k_colpass": " (A^T s11 pass)", "k_rowpass": " (A D pass)",
+                                "k_onepass": " (A D and A^T (A D) in one pass over A)"}[kname]),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"

@@ -21,6 +21,7 @@
 #include "bpgl_host.h"
 #include "bpgl_kernels.h"
 #include "bpgl_fused.h"
+#include "bpgl_onepass.h"
 
 using namespace bpgl;
 
@@ -40,7 +41,7 @@ int fail(int code, const char* fmt, ...) {
 using namespace bpgl_host;
 
 namespace {
-constexpr int kTimedKinds = 7;
+constexpr int kTimedKinds = 8;
 constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
@@ -78,6 +79,15 @@ struct bpgl_ctx {
     int col_mode = 1;      // k_colpass row schedule (see launch_colpass)
     int nt_loads = 1;
     int tail_permille = 120;
+    // one-pass iteration (bpgl_onepass.h)
+    int cus = 256;
+    int onepass = -1;          // tuning: -1 when eligible, 0 off, 1 required
+    int op_refresh = 64;       // exact g = A^T r every this many iterations (0: at reset only)
+    bool op_shape = false;     // the shape admits it (geometry)
+    bool op_on = false;        // this solver run uses it
+    int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0;
+    int64_t op_t = 0;          // iterations enqueued since the solver reset
+    OnePassArgs op{};
 };
 
 namespace {
@@ -103,11 +113,27 @@ void geometry(bpgl_ctx* c) {
     c->R = (int)R;
     c->nchunk = (int)cdiv(c->m, R);
     c->nparts = (int)cdiv(c->wp, kColsPerShrink);
+    // one-pass geometry: SB segment blocks per row, floor(CUs / SB) row groups, one block per CU
+    const int bc = c->dtype == BPGL_F32 ? OnePassGeo<4, float>::BC
+                 : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<2, bf16_t>::BC;
+    const int64_t SB = cdiv(c->wp, bc);
+    c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
+    if (c->op_shape) {
+        int64_t ng = std::min<int64_t>(c->cus / SB, c->m);
+        const int64_t R = cdiv(c->m, ng);
+        ng = cdiv(c->m, R);
+        c->op_SB = (int)SB;
+        c->op_ngroups = (int)ng;
+        c->op_R = (int)R;
+        c->op_xl = (ng % 8 == 0) ? 1 : 0;   // each row group's blocks on one XCD (blockIdx % 8)
+    } else {
+        c->op_SB = c->op_ngroups = c->op_R = c->op_xl = 0;
+    }
 }
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, total;
+    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opS, opUs, opPG, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -126,6 +152,11 @@ Layout layout(const bpgl_ctx* c) {
     L.Ax = k.take(8 * (int64_t)c->nblock * c->m);
     L.diag = k.take(8 * (int64_t)c->nblock * c->wp);
     L.rec = k.take(8 * (int64_t)c->nblock * c->wp);
+    const bool op = c->op_shape;
+    L.opG = k.take(op ? 8 * c->wp : 0);
+    L.opS = k.take(op ? 8 * c->m : 0);
+    L.opUs = k.take(op ? 8 * (int64_t)c->op_ngroups * c->wp : 0);
+    L.opPG = k.take(op ? 8 * c->m * c->op_SB : 0);
     L.total = k.off;
     return L;
 }
@@ -203,18 +234,75 @@ int iter_kernel(bpgl_ctx* c, int which) {
 unsigned rowreduce_blocks(const bpgl_ctx* c) {
     return (unsigned)std::min<int64_t>(cdiv(c->m, kRowsPerReduce), kMaxReduceBlocks);
 }
-int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) {
+int rowreduce_p(bpgl_ctx* c, const Params& q, const double* slab, double* out, int mode) {
     const dim3 g(rowreduce_blocks(c)), b(kThreads);
     // one batch of loads per wave covers the segments: 4 waves x BATCH >= nseg
-    if (c->nseg <= 4) hipLaunchKernelGGL(k_rowreduce<1>, g, b, 0, c->stream, c->p, slab, out, mode);
-    else if (c->nseg <= 16) hipLaunchKernelGGL(k_rowreduce<4>, g, b, 0, c->stream, c->p, slab, out, mode);
-    else hipLaunchKernelGGL(k_rowreduce<16>, g, b, 0, c->stream, c->p, slab, out, mode);
+    if (q.nseg <= 4) hipLaunchKernelGGL(k_rowreduce<1>, g, b, 0, c->stream, q, slab, out, mode);
+    else if (q.nseg <= 16) hipLaunchKernelGGL(k_rowreduce<4>, g, b, 0, c->stream, q, slab, out, mode);
+    else hipLaunchKernelGGL(k_rowreduce<16>, g, b, 0, c->stream, q, slab, out, mode);
     LAUNCH_CHECK("k_rowreduce");
     if (mode == 1) {
-        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, c->p, (int)rowreduce_blocks(c));
+        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, q, (int)rowreduce_blocks(c));
         LAUNCH_CHECK("k_linesearch");
     }
     return 0;
+}
+int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) { return rowreduce_p(c, c->p, slab, out, mode); }
+
+// ---------------------------------------------------------------------------
+// one-pass iteration (bpgl_onepass.h)
+// ---------------------------------------------------------------------------
+// ring slots, rows in flight, 16-byte loads per lane per row (4 KiB fp32 / fp64, 2 KiB bf16
+// per wave and row); profiles/r01/sweeps/onepass6_probe.jsonl
+template <typename T> struct OpCfg { static constexpr int NB = 16, PF = 3, LU = 4; };
+template <> struct OpCfg<bf16_t> { static constexpr int NB = 24, PF = 4, LU = 2; };
+
+template <typename T>
+const void* onepass_fn_t() { return (const void*)k_onepass<T, OpCfg<T>::NB, OpCfg<T>::PF, OpCfg<T>::LU>; }
+const void* onepass_fn(int dtype) {
+    return dtype == BPGL_F32 ? onepass_fn_t<float>() : dtype == BPGL_F64 ? onepass_fn_t<double>() : onepass_fn_t<bf16_t>();
+}
+template <typename T>
+void onepass_launch_t(bpgl_ctx* c) {
+    hipLaunchKernelGGL((k_onepass<T, OpCfg<T>::NB, OpCfg<T>::PF, OpCfg<T>::LU>),
+                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, c->p, c->op);
+}
+int onepass_launch(bpgl_ctx* c) {
+    switch (c->dtype) {
+        case BPGL_F32: onepass_launch_t<float>(c); break;
+        case BPGL_F64: onepass_launch_t<double>(c); break;
+        default: onepass_launch_t<bf16_t>(c); break;
+    }
+    LAUNCH_CHECK("k_onepass");
+    return 0;
+}
+// the two-pass kernels' view of one-pass state: g is read from G (one slab row), s23 from S
+Params op_params(const bpgl_ctx* c) {
+    Params q = c->p;
+    q.slab_g = c->op.G;
+    q.nchunk = 1;
+    q.nseg = 1;
+    return q;
+}
+// exact g = A^T r into G (at reset and every op_refresh iterations)
+int onepass_refresh(bpgl_ctx* c) {
+    int rc;
+    if ((rc = colpass(c, 0, c->p.r, c->p.slab_g, -1))) return rc;
+    hipLaunchKernelGGL(k_colreduce, dim3((unsigned)cdiv(c->wp, kThreads)), dim3(kThreads), 0, c->stream, c->p.slab_g,
+                       c->wp, c->nchunk, c->op.G, (double*)nullptr);
+    LAUNCH_CHECK("k_colreduce");
+    return 0;
+}
+// can this solver run use the one-pass iteration?  (0 yes; else the reason)
+const char* onepass_ineligible(bpgl_ctx* c) {
+    if (!c->op_shape) return "needs one feature block and at most 64 segment blocks per row";
+    if (c->nranks != 1 || c->comm || c->external) return "needs a single rank without a communicator";
+    if (c->fused) return "not combined with the fused iteration";
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype), kThreads, 0) != hipSuccess || nb < 1)
+        return "kernel does not fit on a CU";
+    if ((int64_t)c->op_ngroups * c->op_SB > (int64_t)nb * c->cus) return "grid exceeds the resident capacity";
+    return nullptr;
 }
 
 int check_ready(const bpgl_ctx* c) {
@@ -282,8 +370,39 @@ int finalize_fused(bpgl_ctx* c) {
 // phase 0: colpass, shrink, rowpass, rowreduce [, allreduce, step]; phase 1: update.
 // With the caller doing the exchange (external ranks) phase 0 stops after
 // rowreduce and phase 1 starts with the step.
+// one-pass iteration: shrink (g from G), k_onepass (s23 and U partials), rowreduce of s23
+// + line search; phase 1: x / Ax update and g += gamma U
+int enqueue_phase_onepass(bpgl_ctx* c, int64_t it, int phase) {
+    int rc;
+    if (phase == 0) {
+        const Params q = op_params(c);
+        ev_record(c, it, 1, 0);
+        hipLaunchKernelGGL(k_shrink, dim3((unsigned)c->nparts), dim3(kThreads), 0, c->stream, q);
+        LAUNCH_CHECK("k_shrink");
+        ev_record(c, it, 1, 1);
+        ev_record(c, it, 7, 0);
+        if ((rc = onepass_launch(c))) return rc;
+        ev_record(c, it, 7, 1);
+        ev_record(c, it, 3, 0);
+        if ((rc = rowreduce_p(c, q, c->op.S, c->p.comm, 1))) return rc;
+        ev_record(c, it, 3, 1);
+    } else {
+        ev_record(c, it, 6, 0);
+        const int64_t nupd = std::max<int64_t>(c->wp, c->m);
+        const unsigned ublocks = (unsigned)std::min<int64_t>(cdiv(nupd, kThreads), 1024);
+        hipLaunchKernelGGL(k_update, dim3(ublocks), dim3(kThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_update");
+        hipLaunchKernelGGL(k_onepass_gupdate, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024)),
+                           dim3(kThreads), 0, c->stream, c->p, c->op);
+        LAUNCH_CHECK("k_onepass_gupdate");
+        ev_record(c, it, 6, 1);
+    }
+    return 0;
+}
+
 int enqueue_phase(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
+    if (c->op_on) return enqueue_phase_onepass(c, it, phase);
     if (c->fused) return enqueue_phase_fused(c, it, phase);
     const bool multi = c->comm != nullptr || c->external;
     if (phase == 0) {
@@ -359,6 +478,9 @@ int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_lo
     c->n_local = n_local;
     c->nblock = nblock;
     c->w = n_local / nblock;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->cus = cus;
     if (hip_stream) {
         c->stream = (hipStream_t)hip_stream;
     } else {
@@ -456,7 +578,19 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     p.diag = (const double*)(s + L.diag);
     p.rec = (const double*)(s + L.rec);
     p.wall_tick_s = c->wall_tick_s;
+    c->op = OnePassArgs{};
+    if (c->op_shape) {
+        c->op.G = (double*)(s + L.opG);
+        c->op.S = (double*)(s + L.opS);
+        c->op.Us = (double*)(s + L.opUs);
+        c->op.PG = (unsigned long long*)(s + L.opPG);
+        c->op.SB = c->op_SB;
+        c->op.ngroups = c->op_ngroups;
+        c->op.R = c->op_R;
+        c->op.xl = c->op_xl;
+    }
     HIP_TRY(hipSetDevice(c->device));
+    if (c->op_shape) HIP_TRY(hipMemsetAsync(s + L.opPG, 0, 8 * c->m * c->op_SB, c->stream));   // tag 0: never written
     HIP_TRY(hipMemsetAsync(s + L.st, 0, sizeof(DevState), c->stream));
     HIP_TRY(hipMemsetAsync(s + L.D, 0, 8 * c->wp, c->stream));
     HIP_TRY(hipMemsetAsync(s + L.Dbuf, 0, 16 * c->wp, c->stream));
@@ -610,6 +744,13 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
     hipLaunchKernelGGL(k_reset, dim3((unsigned)std::min<int64_t>(cdiv(c->m, kThreads), 1024)), dim3(kThreads), 0,
                        c->stream, p);
     LAUNCH_CHECK("k_reset");
+    {
+        const char* why = c->onepass != 0 ? onepass_ineligible(c) : "disabled";
+        if (c->onepass == 1 && why) return fail(BPGL_E_ARG, "onepass=1: %s", why);
+        c->op_on = c->onepass != 0 && !why;
+        c->op_t = 0;
+        if (c->op_on && (rc = onepass_refresh(c))) return rc;
+    }
     drop_graphs(c);
     c->use_graph = use_graph != 0 && !c->external;
     if (c->use_graph) {
@@ -642,16 +783,22 @@ int bpgl_solver_step(bpgl_ctx* c, int64_t n_iter) {
     if (n_iter < 0) return fail(BPGL_E_ARG, "n_iter < 0");
     if (c->external) return fail(BPGL_E_STATE, "external-exchange ranks advance with bpgl_solver_phase");
     HIP_TRY(hipSetDevice(c->device));
-    int64_t i = 0;
-    if (!c->timing && c->gexec_k)
-        for (; i + kGraphIters <= n_iter; i += kGraphIters) HIP_TRY(hipGraphLaunch(c->gexec_k, c->stream));
-    for (; i < n_iter; ++i) {
-        if (c->timing || !c->gexec) {
+    const int64_t K = c->op_on ? c->op_refresh : 0;
+    for (int64_t i = 0; i < n_iter;) {
+        if (K > 0 && c->op_t > 0 && c->op_t % K == 0 && (rc = onepass_refresh(c))) return rc;
+        const int64_t room = K > 0 ? std::min<int64_t>(n_iter - i, K - c->op_t % K) : n_iter - i;
+        int64_t k = 1;
+        if (!c->timing && c->gexec_k && room >= kGraphIters) {
+            HIP_TRY(hipGraphLaunch(c->gexec_k, c->stream));
+            k = kGraphIters;
+        } else if (c->timing || !c->gexec) {
             if ((rc = enqueue_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
             if (c->timing) c->timed_iters++;
         } else {
             HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
         }
+        i += k;
+        c->op_t += k;
     }
     return finalize_fused(c);
 }
@@ -669,6 +816,9 @@ int bpgl_solver_status(bpgl_ctx* c, int64_t* iters_done, int* stopped, int64_t* 
     if (t_last) *t_last = st.t_last;
     if (gamma) *gamma = st.gamma;
     if (err) *err = st.err;
+    if (st.op_fail)
+        return fail(BPGL_E_EXCHANGE, "one-pass row hand-off timed out (another kernel held CUs while k_onepass "
+                                     "ran); reset the solver");
     return 0;
 }
 
@@ -713,6 +863,18 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->fused = value != 0;
         drop_graphs(c);
         c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "onepass")) {
+        if (value < -1 || value > 1) return fail(BPGL_E_ARG, "onepass must be -1, 0 or 1");
+        c->onepass = (int)value;
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "onepass_refresh")) {
+        if (value < 0) return fail(BPGL_E_ARG, "onepass_refresh must be >= 0");
+        c->op_refresh = (int)std::min<int64_t>(value, 1 << 30);
         return 0;
     }
     if (!strcmp(key, "nt_loads")) {

@@ -38,10 +38,11 @@ struct DevState {
     double err;           // error criterion of the last iteration
     double r1, r2;        // line-search numerators (diagnostics)
     long long iters;      // iterations completed (update applied or stop reached)
-    unsigned long long reserved0;
+    unsigned long long op_ran;   // one-pass mode: k_onepass ran in this iteration (advances op_epoch)
     long long pending;    // fused mode: the update of iteration t-1 is not yet applied to x / Ax
     unsigned long long cnt_all;         // fused mode: arrivals of row-chunk finishers in k_iter_b
-    long long pad[2];
+    long long op_epoch;   // one-pass mode: launches so far (tag of the row-partial hand-off)
+    long long op_fail;    // one-pass mode: a hand-off poll ran out (blocks not co-resident)
 };
 
 struct Params {
@@ -734,7 +735,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(Params p) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         DevState* st = p.st;
         st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0; st->pending = 0;
-        st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0;
+        st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0; st->op_fail = 0;
         st->t_base = (long long)wall_clock64();
         if (p.time_iter) p.time_iter[0] = 0.0;
     }

@@ -1,0 +1,254 @@
+// One-HBM-pass iteration (single feature block, single rank): A is streamed once per
+// iteration and yields both products the iteration needs.
+//
+// For one block the gradient obeys the recurrence
+//     g_{t+1} = A^T r_{t+1} = A^T (r_t + gamma_t s23_t) = g_t + gamma_t A^T (A D_t)
+// (the reference applies the same update to Ax, lasso.py:155).  So an iteration needs
+// s23 = A D and U = A^T s23 -- two passes over A if done one after the other, but only one
+// if every row's s23 is complete while the row is still on chip.  k_onepass does that:
+//
+//   * grid = ngroups x SB persistent blocks (one per CU, all resident): a row group of SB
+//     segment blocks walks the same R rows; block sb owns 4 x WC columns, wave q of the
+//     block WC of them (WC = 64 lanes x LU 16-byte loads);
+//   * per row t each wave keeps the row in registers: phase 1 forms its partial of
+//     s23[t] (fp64 FMA, DPP row sums), stores it in an LDS slot; wave t % 4 folds the 4
+//     slots in a fixed order and publishes ONE granule per (row, block): the fp64 partial
+//     with its lowest mantissa bit replaced by the launch parity, one 8-byte agent-scope
+//     store (a single-copy-atomic hand-off, no fences).  One bit suffices: every launch
+//     that runs rewrites every granule, so a reader sees this launch's value or the
+//     previous launch's, and consecutive launches alternate parity (op_epoch advances
+//     exactly when k_onepass ran);
+//   * LAG rows later (the row is still in the register ring) every wave reads the SB
+//     granules of row t (lane = block; the load was issued PF rows earlier beside the row
+//     prefetch, so the in-order vmcnt queue is never drained), checks their tags and folds
+//     them in one fixed order -> s23[t], bit-identical in every block; U += row * s23[t];
+//   * a late granule is re-polled (bounded; on exhaustion the state's op_fail word is set
+//     and the kernel still finishes -- bpgl_solver_status reports BPGL_E_EXCHANGE).
+// Outputs: s23 (by segment block 0) and one U partial row per row group; k_onepass_gupdate
+// folds the partials in a fixed order into g += gamma U after the line search.  Results are
+// bitwise deterministic; the tag bit perturbs each s23 partial by <= 1 ulp (2^-52 relative).
+// Measured development steps: tools/onepass*_probe.hip, DESIGN.md section 6b.
+#pragma once
+#include "bpgl_kernels.h"
+
+namespace bpgl {
+
+constexpr int kOpSlotsLog = 5;
+constexpr int kOpSlots = 1 << kOpSlotsLog;   // LDS partial slots (rows); > LAG + publication delay
+// an LDS slot's parity: row t and the slot's previous row t - kOpSlots differ in bit kOpSlotsLog
+constexpr int kOpDelta = 1;     // rows between a row's phase 1 and its publication
+constexpr int kOpMaxSB = 64;    // one granule per lane
+constexpr unsigned kOpPolls = 1u << 16;
+
+struct OnePassArgs {
+    double* G;                   // [wp]   gradient carried across iterations
+    double* S;                   // [m]    s23 = A D
+    double* Us;                  // [ngroups][wp] U partial of each row group
+    unsigned long long* PG;      // [m][SB] tagged row partials
+    int SB, ngroups, R, xl;      // segment blocks per row, row groups, rows per group, XCD-local map
+};
+
+typedef unsigned long long op_u64;
+
+// a hand-off word: fp64 value with its lowest mantissa bit replaced by a parity tag
+__device__ __forceinline__ op_u64 op_stuff(double x, unsigned bit) {
+    return ((op_u64)__double_as_longlong(x) & ~1ull) | (bit & 1u);
+}
+__device__ __forceinline__ double op_unstuff(op_u64 g) { return __longlong_as_double((long long)(g & ~1ull)); }
+__device__ __forceinline__ unsigned op_tag(op_u64 g) { return (unsigned)(g & 1ull); }
+
+// DPP lane exchange: a VALU op, no LDS round trip (with one wave per SIMD the ds_bpermute
+// latency of __shfl_xor chains is not hidden by other waves)
+template <int CTRL>
+__device__ __forceinline__ double op_dpp(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// sum over each 16-lane row, the same bits in every lane of the row: each level adds an
+// equally shaped partner group, and fp addition is commutative
+__device__ __forceinline__ double op_row_sum16(double x) {
+    x += op_dpp<0xb1>(x);    // quad_perm [1,0,3,2]
+    x += op_dpp<0x4e>(x);    // quad_perm [2,3,0,1]
+    x += op_dpp<0x141>(x);   // row_half_mirror
+    x += op_dpp<0x140>(x);   // row_mirror
+    return x;
+}
+__device__ __forceinline__ double op_lane(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// wave sum in a fixed order, uniform result: 16-lane rows, then (r0 + r1) + (r2 + r3)
+__device__ __forceinline__ double op_wave_sum(double x) {
+    x = op_row_sum16(x);
+    return (op_lane(x, 0) + op_lane(x, 16)) + (op_lane(x, 32) + op_lane(x, 48));
+}
+
+template <int LU, typename T>
+struct OnePassGeo {
+    static constexpr int N = VecT<T>::N;
+    static constexpr int CPL = LU * N;       // columns per lane
+    static constexpr int WC = 64 * CPL;      // columns per wave
+    static constexpr int BC = kWaves * WC;   // columns per segment block
+};
+
+template <typename T, int NB, int PF, int LU>
+__global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o) {
+    if (p.st->done) return;
+    using G = OnePassGeo<LU, T>;
+    using raw = typename VecT<T>::raw;
+    constexpr int N = G::N;
+    constexpr int LAG = NB - PF - 1;
+    static_assert(LAG > PF + kOpDelta && LAG + kOpDelta < kOpSlots, "ring geometry");
+    __shared__ op_u64 part[kOpSlots][kWaves];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x, SB = o.SB;
+    int grp, sb;
+    if (o.xl) { grp = (b & 7) + 8 * ((b >> 3) / SB); sb = (b >> 3) % SB; }
+    else { grp = b / SB; sb = b % SB; }
+    const long long i0 = (long long)grp * o.R;
+    const long long i1 = i0 + o.R < p.m ? i0 + o.R : p.m;
+    const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
+    if (nrows == 0) return;   // the whole row group (uniform)
+    const unsigned tag = (unsigned)((p.st->op_epoch + 1) & 1);   // bound scratch is zero: parity 0 = unwritten
+    if (b == 0 && threadIdx.x == 0) p.st->op_ran = 1;
+
+    for (int k = threadIdx.x; k < kOpSlots * kWaves; k += kThreads) (&part[0][0])[k] = 1ull;   // rows 0..31: parity 0
+    __syncthreads();
+
+    // this lane's columns: LU 16-byte groups, 64 * N apart
+    const T* __restrict__ Ab = reinterpret_cast<const T*>(p.A);
+    long long col[LU];
+    double d[LU][N], u[LU][N];
+    bool colok[LU];
+#pragma unroll
+    for (int k = 0; k < LU; ++k) {
+        const long long c = (long long)sb * G::BC + wave * G::WC + k * 64 * N + lane * N;
+        colok[k] = c < p.wp;
+        col[k] = colok[k] ? c : 0;
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+            d[k][e] = colok[k] ? p.D[c + e] : 0.0;
+            u[k][e] = 0.0;
+        }
+    }
+    const int glane = lane < SB ? lane : 0;
+    raw buf[NB][LU];
+    op_u64 gv[NB];
+    unsigned polls = kOpPolls;
+    bool failed = false;
+
+    auto load = [&](int t, int slot) {
+        const int tc = t < nrows ? t : nrows - 1;
+        const T* rp = Ab + (i0 + tc) * p.lda;
+#pragma unroll
+        for (int k = 0; k < LU; ++k) buf[slot][k] = ldv<T, true>(rp + col[k]);
+    };
+    auto gload = [&](int t, int slot) {   // granules consumed at step t (phase 2 of row t - LAG)
+        int t2 = t - LAG;
+        t2 = t2 < 0 ? 0 : (t2 >= nrows ? nrows - 1 : t2);
+        gv[slot] = __hip_atomic_load(o.PG + (i0 + t2) * SB + glane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+
+#pragma unroll
+    for (int q = 0; q < PF; ++q) { gload(q, q); load(q, q); }
+    for (int base = 0; base < nrows + LAG; base += NB) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int t = base + q;
+            const int qn = (q + PF) % NB;
+            gload(t + PF, qn);
+            load(t + PF, qn);
+            if (t < nrows) {   // phase 1: this wave's partial of s23[t] into its LDS slot
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k < LU; ++k) {
+                    double v[N];
+                    VecT<T>::cvt(buf[q][k], v);
+#pragma unroll
+                    for (int e = 0; e < N; ++e) s = fma(v[e], d[k][e], s);
+                }
+                s = op_wave_sum(s);
+                if (lane == 0)
+                    __hip_atomic_store(&part[t % kOpSlots][wave], op_stuff(s, (unsigned)t >> kOpSlotsLog),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            const int tp = t - kOpDelta;   // publication of row tp by wave tp % 4
+            if (tp >= 0 && tp < nrows && (tp & 3) == wave) {
+                const unsigned want = ((unsigned)tp >> kOpSlotsLog) & 1u;
+                op_u64 w = 0;
+                while (true) {
+                    w = lane < kWaves ? __hip_atomic_load(&part[tp % kOpSlots][lane], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP)
+                                      : 0;
+                    if (__all(lane >= kWaves || op_tag(w) == want)) break;
+                    if (polls == 0) { failed = true; break; }
+                    --polls;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                const double x = op_unstuff(w);
+                const double bsum = (op_lane(x, 0) + op_lane(x, 1)) + (op_lane(x, 2) + op_lane(x, 3));
+                if (lane == 0)
+                    __hip_atomic_store(o.PG + (i0 + tp) * SB + sb, op_stuff(bsum, tag), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const int t2 = t - LAG;
+            if (t2 >= 0 && t2 < nrows) {   // phase 2: U += row(t2) * s23[t2]
+                const int qs = (q - LAG + NB) % NB;
+                op_u64 v = gv[q];
+                auto ready = [&](op_u64 g) { return lane >= SB || op_tag(g) == tag; };
+                if (!__all(ready(v))) {   // late: re-poll (drains this wave's queue; rare)
+                    const op_u64* src = o.PG + (i0 + t2) * SB + glane;
+                    do {
+                        if (polls == 0) { failed = true; break; }
+                        --polls;
+                        __builtin_amdgcn_s_sleep(2);
+                        v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } while (!__all(ready(v)));
+                    // settle here, so the merge with the fast path is not a pending load
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    asm volatile("" : "+v"(v));
+                }
+                double x = lane < SB ? op_unstuff(v) : 0.0;
+                x = SB <= 16 ? op_lane(op_row_sum16(x), 0) : op_wave_sum(x);
+                if (sb == 0 && wave == 0 && lane == 0) o.S[i0 + t2] = x;
+#pragma unroll
+                for (int k = 0; k < LU; ++k) {
+                    double v2[N];
+                    VecT<T>::cvt(buf[qs][k], v2);
+#pragma unroll
+                    for (int e = 0; e < N; ++e) u[k][e] = fma(v2[e], x, u[k][e]);
+                }
+            }
+        }
+    }
+    if (failed && lane == 0) atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
+    double* dst = o.Us + (long long)grp * p.wp;
+#pragma unroll
+    for (int k = 0; k < LU; ++k)
+        if (colok[k])
+#pragma unroll
+            for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
+}
+
+// g += gamma * sum_groups Us (fixed order) after the line search; advances the launch
+// parity iff k_onepass ran (it also runs in the iteration whose line search stops)
+__global__ __launch_bounds__(kThreads) void k_onepass_gupdate(Params p, OnePassArgs o) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && p.st->op_ran) {
+        p.st->op_epoch += 1;
+        p.st->op_ran = 0;
+    }
+    if (p.st->done) return;
+    const double gamma = p.st->gamma;
+    for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < p.wp; j += (long long)gridDim.x * kThreads) {
+        double acc = 0.0;
+        for (int g = 0; g < o.ngroups; ++g) acc += o.Us[(long long)g * p.wp + j];
+        o.G[j] += gamma * acc;
+    }
+}
+
+}  // namespace bpgl

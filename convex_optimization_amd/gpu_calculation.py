@@ -279,10 +279,10 @@ class GPU_Calculation:
     def set_kernel_timing(self, enable):
         N.check(N.lib().bpgl_set_kernel_timing(self._ctx, int(bool(enable))), "bpgl_set_kernel_timing")
 
-    KERNEL_KINDS = ("colpass", "shrink", "rowpass", "rowreduce", "allreduce", "step", "update")
+    KERNEL_KINDS = ("colpass", "shrink", "rowpass", "rowreduce", "allreduce", "step", "update", "onepass")
 
     def kernel_times(self):
-        arr = (ctypes.c_double * 7)()
+        arr = (ctypes.c_double * len(self.KERNEL_KINDS))()
         ns = ctypes.c_int64()
         N.check(N.lib().bpgl_kernel_times(self._ctx, arr, ctypes.byref(ns)), "bpgl_kernel_times")
         return dict(zip(self.KERNEL_KINDS, list(arr))), ns.value

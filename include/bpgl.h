@@ -39,7 +39,10 @@ enum {
     BPGL_E_STATE = -2,    /* call out of order (not bound / no solver)   */
     BPGL_E_HIP = -3,      /* HIP runtime error                           */
     BPGL_E_RCCL = -4,     /* RCCL error                                  */
-    BPGL_E_SCRATCH = -5   /* scratch buffer too small                    */
+    BPGL_E_SCRATCH = -5,  /* scratch buffer too small                    */
+    BPGL_E_EXCHANGE = -6  /* one-pass row hand-off timed out (another
+                             kernel held CUs); the solver state is
+                             invalid until the next bpgl_solver_reset     */
 };
 
 typedef struct bpgl_ctx bpgl_ctx;
@@ -160,18 +163,32 @@ int bpgl_iterate(bpgl_ctx* ctx, int64_t n_iter, const int32_t* order, double mu,
  * average duration (ms) of each kernel kind over the window, measured with
  * HIP events when profiling was enabled by bpgl_set_kernel_timing(ctx, 1).
  * kinds: 0 colpass (A^T r), 1 shrink, 2 rowpass (A D), 3 rowreduce (+ line
- * search on one rank), 4 allreduce, 5 step (multi-rank line search), 6 update. */
+ * search on one rank), 4 allreduce, 5 step (multi-rank line search), 6 update
+ * (+ gradient update in one-pass mode), 7 onepass (A D and A^T (A D) in one
+ * pass over A). */
 int bpgl_set_kernel_timing(bpgl_ctx* ctx, int enable);
-int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 7 */, int64_t* samples);
+int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
 
-/* Runtime tuning knobs (call before bpgl_solver_reset); none changes results:
+/* Runtime tuning knobs (call before bpgl_solver_reset).  These do not change
+ * results:
  *   "nt_loads" (default 1): stream A with non-temporal loads.
  *   "tail_permille" (default 120): with nt_loads, the share of every row chunk
  *   each pass reads last with cache-allocating loads (Infinity Cache reuse by
  *   the other pass).
  *   "reverse_rows" (default 0): the A D pass walks each row chunk bottom-up.
+ * These select the iteration's arithmetic path (results agree to rounding,
+ * each path is bitwise deterministic):
+ *   "onepass" (default -1 = when eligible, 0 = off, 1 = required): one pass
+ *   over A per iteration, the gradient carried as g += gamma A^T (A D); needs
+ *   one feature block, one rank, no fused mode, at most 64 x 4096 columns
+ *   (fp32/bf16; 64 x 2048 for fp64) and all of its blocks resident at once
+ *   (nothing else running on the device).
+ *   "onepass_refresh" (default 64; 0 = only at reset): recompute g = A^T r
+ *   exactly every this many iterations (bounds the recurrence's drift).
+ *   "fused" (default 0): the two-launch fused iteration.
  * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the
- * number of (row chunk x column segment) tiles per pass (default 2048). */
+ * number of (row chunk x column segment) tiles per two-pass launch (default
+ * 1024 for fp32 A, 512 for fp64 / bf16). */
 int bpgl_set_tuning(bpgl_ctx* ctx, const char* key, int64_t value);
 
 /* Launch geometry chosen for this context (diagnostics). */

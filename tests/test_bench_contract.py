@@ -31,6 +31,16 @@ def test_pass_bytes_and_panel_figures():
     assert b.panel_bytes_pass(8192, 65536, 128) == 2 * 8192 * 65536 + 8 * 128 * (8192 + 65536)
 
 
+def test_onepass_bytes():
+    """one pass over A per iteration: the same vector I/O, A read once (roofline ~3720 it/s)"""
+    b = _bench()
+    it = b.alg_bytes_iter_onepass(8192, 65536)
+    assert it == 8192 * 65536 * 4 + 8 * (5 * 65536 + 5 * 8192)
+    assert it < b.alg_bytes_iter(8192, 65536) / 1.99
+    assert abs(b.HBM_PEAK_GBS * 1e9 / it - 3720) < 1.0
+    assert b.alg_bytes_onepass(8192, 65536) == 8192 * 65536 * 4 + 8 * 8192 + 16 * 65536
+
+
 def test_default_arguments_are_the_headline_config():
     b = _bench()
     import sys
@@ -41,4 +51,5 @@ def test_default_arguments_are_the_headline_config():
     finally:
         sys.argv = argv
     assert (a.gpus, a.m, a.n_per_gpu, a.block, a.type, a.rhs) == (1, 8192, 65536, 1, "float", 1)
+    assert a.onepass == -1   # the library's choice: one pass when eligible
     assert a.steps > 0 and a.warmup >= 0

@@ -1,0 +1,170 @@
+"""One-pass iteration (bpgl_onepass.h): A streamed once per iteration, the gradient
+carried as g += gamma A^T (A D).  Same algorithm as the two-pass iteration
+(lasso.py:102-157); the arithmetic differs by summation order, by <= 1 ulp per hand-off
+partial (the parity bit) and by the recurrence's accumulated rounding between exact
+refreshes (every 64 iterations by default).  Tolerances, relative l2 on x:
+  * a few iterations: <= 1e-12 against the two-pass path (measured ~1e-15);
+  * 25 iterations of random problems: <= 1e-8 (measured 1e-15 .. 3e-9: these lasso
+    trajectories amplify rounding -- the two-pass path itself drifts 6e-10 from the
+    oracle on the worst shape);
+  * the reference's own fixtures: <= 1e-9, as every other solver test;
+  * north_star's bound 1e-5 at the full benchmark shape (measured ~1e-13).
+Results are bitwise deterministic (graph = eager = split steps)."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from convex_optimization_amd import _native as N  # noqa: E402
+from convex_optimization_amd.gpu_calculation import GPU_Calculation  # noqa: E402
+
+
+def make_cls(type_name):
+    return type("GC_" + type_name, (GPU_Calculation,), {"TYPE": type_name})
+
+
+def rel(a, b):
+    a, b = np.asarray(a).reshape(-1), np.asarray(b).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def both(gc, b, mu, iters, **kw):
+    out = {}
+    for op in (1, 0):
+        gc.set_tuning("onepass", op)
+        out[op] = gc.run(b, mu, iters, **kw)
+    gc.set_tuning("onepass", -1)
+    return out[1], out[0]
+
+
+def used_onepass(gc, b, mu):
+    """kernel timing shows which iteration ran"""
+    gc.solver_reset(b, mu, use_graph=False)
+    gc.set_kernel_timing(True)
+    gc.solver_step(2)
+    t, n = gc.kernel_times()
+    gc.set_kernel_timing(False)
+    return t["onepass"] > 0 and t["rowpass"] == 0 and t["colpass"] == 0
+
+
+@pytest.mark.parametrize("case,type_name", [("c1_b1_p1_f32in", "float"), ("c1_b1_p1_f32in", "double"),
+                                            ("c1_b1_p1_f64", "double")])
+def test_reference_fixture(golden, case, type_name):
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    IT = int(fx["ITER_MAX"])
+    gc = make_cls(type_name)(A, 1, device=0)
+    eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
+    assert used_onepass(gc, fx["b"], float(fx["mu"]))   # the default for one block on one rank
+    one, two = both(gc, fx["b"], float(fx["mu"]), IT, err_bound=eb, record=True)
+    for res in (one, two):
+        assert res["t_last"] == int(fx["t_last"])
+        assert res["stopped"] == bool(fx["stopped"])
+        assert rel(res["x"], fx["x"]) <= 1e-9
+    assert rel(one["x"], two["x"]) <= 1e-10, rel(one["x"], two["x"])
+    T = int(fx["t_last"]) + 1
+    np.testing.assert_allclose(one["err_iter"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
+
+
+# (m, n, dtype): ragged widths (not a multiple of the 4096-column segment block), fewer
+# rows than row groups, many row groups, 64 segment blocks per row, tiny problems
+SHAPES = [(1000, 4100, "float"), (37, 9000, "float"), (4099, 1536, "float"), (256, 262144, "float"),
+          (3, 5, "float"), (2048, 8192, "double"), (777, 3000, "double"), (1500, 10000, "bf16"),
+          (300, 64 * 4096, "bf16"), (64, 2048 * 64, "double")]
+
+
+@pytest.mark.parametrize("m,n,type_name", SHAPES)
+def test_shapes_match_two_pass_and_oracle(m, n, type_name):
+    rs = np.random.RandomState(m + 7 * n)
+    A = rs.randn(m, n) / np.sqrt(n)
+    x_true = np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0)
+    b = A @ x_true + 0.01 * rs.randn(m)
+    mu = 0.1 * np.abs(A.T @ b).max()
+    gc = make_cls(type_name)(A, 1, device=0)
+    assert used_onepass(gc, b, mu)
+    one, two = both(gc, b, mu, 5)
+    assert rel(one["x"], two["x"]) <= 1e-12, rel(one["x"], two["x"])
+    IT = 25
+    one, two = both(gc, b, mu, IT)
+    assert rel(one["x"], two["x"]) <= 1e-8, rel(one["x"], two["x"])
+    assert one["t_last"] == two["t_last"]
+    if m * n <= 4_000_000:
+        Ah = gc.A_b_gpu[0, :, :n].to(torch.float64).cpu().numpy()
+        ref = oracle.run(np.ascontiguousarray(Ah), b, mu, 1, IT)
+        assert rel(one["x"], ref["x"]) <= 1e-8, rel(one["x"], ref["x"])
+
+
+def test_graph_eager_split_steps_bitwise():
+    rs = np.random.RandomState(5)
+    A = rs.randn(900, 5000)
+    b = rs.randn(900)
+    gc = make_cls("float")(A, 1, device=0)
+    mu = 0.05 * float(np.abs(A.T @ b).max())
+    a = gc.run(b, mu, 90, use_graph=True)["x"]
+    e = gc.run(b, mu, 90, use_graph=False)["x"]
+    c = gc.run(b, mu, 90, use_graph=True)["x"]
+    np.testing.assert_array_equal(a, e)
+    np.testing.assert_array_equal(a, c)
+    gc.solver_reset(b, mu)
+    for k in (3, 17, 8, 62):   # crosses the refresh points 64 and 0 in different graph phases
+        gc.solver_step(k)
+    np.testing.assert_array_equal(gc.solver_x(), gc.run(b, mu, 90)["x"])
+
+
+@pytest.mark.parametrize("refresh", [0, 1, 5, 64])
+def test_refresh_period(refresh):
+    """the gradient recurrence with and without exact refreshes: same iterates to rounding"""
+    rs = np.random.RandomState(9)
+    A = rs.randn(1200, 6000)
+    b = rs.randn(1200)
+    mu = 0.05 * float(np.abs(A.T @ b).max())
+    gc = make_cls("float")(A, 1, device=0)
+    gc.set_tuning("onepass", 0)
+    two = gc.run(b, mu, 150)
+    gc.set_tuning("onepass", 1)
+    gc.set_tuning("onepass_refresh", refresh)
+    one = gc.run(b, mu, 150)
+    assert rel(one["x"], two["x"]) <= 1e-8, rel(one["x"], two["x"])
+
+
+def test_stop_rule_and_restart():
+    """err_bound stop: same t_last as two-pass; a reset after a stop runs clean (fresh tags)"""
+    rs = np.random.RandomState(4)
+    A = rs.randn(600, 3000)
+    b = A @ np.where(rs.rand(3000) < 0.1, rs.randn(3000), 0.0)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    gc = make_cls("float")(A, 1, device=0)
+    one, two = both(gc, b, mu, 400, err_bound=1e-3)
+    assert one["stopped"] and two["stopped"] and one["t_last"] == two["t_last"]
+    again = gc.run(b, mu, 400, err_bound=1e-3)
+    np.testing.assert_array_equal(again["x"], one["x"])
+
+
+def test_required_but_ineligible_raises():
+    A = np.random.RandomState(0).randn(64, 256)
+    gc = make_cls("float")(A, 2, device=0)      # two feature blocks
+    gc.set_tuning("onepass", 1)
+    with pytest.raises(N.BpglError, match="onepass=1"):
+        gc.run(np.ones(64), 0.1, 3)
+    gc.set_tuning("onepass", -1)
+    assert gc.run(np.ones(64), 0.1, 3)["iters"] == 3   # auto falls back to two passes
+    with pytest.raises(N.BpglError):
+        gc.set_tuning("onepass", 2)
+
+
+def test_full_size_matches_oracle():
+    """configs[1] (8192 x 65536 fp32): one pass per iteration vs the oracle"""
+    from convex_optimization_amd.parameters import device_instance
+    gc, b, mu, _ = device_instance(8192, 65536, 0.4, 1, TYPE="float", seed=11, device=0)
+    assert used_onepass(gc, b, mu)
+    res = gc.run(b, mu, 8)
+    A_host = gc.A_b_gpu[0].cpu().numpy()
+    ref = oracle.run(np.ascontiguousarray(A_host), b.cpu().numpy(), mu, 1, 8, nthreads=16)
+    assert rel(res["x"], ref["x"]) <= 1e-5
+    assert rel(res["x"], ref["x"]) <= 1e-10, rel(res["x"], ref["x"])

@@ -38,6 +38,10 @@ def per_launch(dirname, counter):
                     key = "k_colpass"
                 elif "k_rowpass" in name:
                     key = "k_rowpass"
+                elif "k_onepass_gupdate" in name:
+                    continue
+                elif "k_onepass" in name:
+                    key = "k_onepass"
                 elif "k_panel_pass1" in name:
                     key = "k_panel_pass1"
                 elif "k_panel_pass2" in name:

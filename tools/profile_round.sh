@@ -12,10 +12,10 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -- \
     python3 $R/bench.py --steps 50 --warmup 10 --no-cpu > $OUT/bench_trace.json 2> $OUT/trace.err
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch \
-    --kernel-include-regex "k_iter_a|k_iter_b|k_colpass|k_rowpass" -- \
+    --kernel-include-regex "k_iter_a|k_iter_b|k_colpass|k_rowpass|k_onepass" -- \
     python3 $R/bench.py --steps 6 --warmup 2 --no-cpu > $OUT/bench_fetch.json 2> $OUT/fetch.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write \
-    --kernel-include-regex "k_iter_a|k_iter_b|k_colpass|k_rowpass" -- \
+    --kernel-include-regex "k_iter_a|k_iter_b|k_colpass|k_rowpass|k_onepass" -- \
     python3 $R/bench.py --steps 6 --warmup 2 --no-cpu > $OUT/bench_write.json 2> $OUT/write.err
 cd $R
 python3 tools/pmc_traffic.py $OUT/fetch $OUT/write m8192_n65536_b1_float_g1 $((8192*65536*4 + 8*8192 + 8*65536))
