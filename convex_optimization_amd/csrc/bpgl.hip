@@ -83,9 +83,10 @@ struct bpgl_ctx {
     int cus = 256;
     int onepass = -1;          // tuning: -1 when eligible, 0 off, 1 required
     int op_refresh = 64;       // exact g = A^T r every this many iterations (0: at reset only)
+    int op_variant = 0;        // ring depth / prefetch variant (OpVar)
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
-    int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0;
+    int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0;
     int64_t op_t = 0;          // iterations enqueued since the solver reset
     OnePassArgs op{};
 };
@@ -126,14 +127,15 @@ void geometry(bpgl_ctx* c) {
         c->op_ngroups = (int)ng;
         c->op_R = (int)R;
         c->op_xl = (ng % 8 == 0) ? 1 : 0;   // each row group's blocks on one XCD (blockIdx % 8)
+        c->op_tail_grid = (int)std::min<int64_t>(cdiv(std::max<int64_t>(c->m, c->wp), kThreads), kOpTailBlocks);
     } else {
-        c->op_SB = c->op_ngroups = c->op_R = c->op_xl = 0;
+        c->op_SB = c->op_ngroups = c->op_R = c->op_xl = c->op_tail_grid = 0;
     }
 }
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opS, opUs, opPG, total;
+    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opUs, opPG, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -143,7 +145,7 @@ Layout layout(const bpgl_ctx* c) {
     L.slab_s = k.take(8 * (int64_t)c->nseg * c->m);
     L.g = k.take(8 * c->wp);
     L.D = k.take(8 * c->wp);
-    L.parts = k.take(8 * 4 * (int64_t)c->nparts);
+    L.parts = k.take(8 * 4 * (int64_t)std::max(c->nparts, c->op_tail_grid));
     L.parts2 = k.take(8 * 2 * std::max<int64_t>(kMaxReduceBlocks, c->nchunk));
     L.Dbuf = k.take(8 * 2 * c->wp);
     L.cnt = k.take(8 * ((int64_t)c->nseg + c->nchunk));
@@ -154,7 +156,6 @@ Layout layout(const bpgl_ctx* c) {
     L.rec = k.take(8 * (int64_t)c->nblock * c->wp);
     const bool op = c->op_shape;
     L.opG = k.take(op ? 8 * c->wp : 0);
-    L.opS = k.take(op ? 8 * c->m : 0);
     L.opUs = k.take(op ? 8 * (int64_t)c->op_ngroups * c->wp : 0);
     L.opPG = k.take(op ? 8 * c->m * c->op_SB : 0);
     L.total = k.off;
@@ -252,20 +253,50 @@ int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) { return r
 // ---------------------------------------------------------------------------
 // one-pass iteration (bpgl_onepass.h)
 // ---------------------------------------------------------------------------
-// ring slots, rows in flight, 16-byte loads per lane per row (4 KiB fp32 / fp64, 2 KiB bf16
-// per wave and row); profiles/r01/sweeps/onepass6_probe.jsonl
-template <typename T> struct OpCfg { static constexpr int NB = 16, PF = 3, LU = 4; };
-template <> struct OpCfg<bf16_t> { static constexpr int NB = 24, PF = 4, LU = 2; };
+// ring slots NB and rows in flight PF per variant (tuning key "onepass_variant"); the loads
+// per lane and row (LU: 4 KiB of fp32 / fp64, 2 KiB of bf16 A per wave and row) are fixed per
+// storage type because they set the geometry.  profiles/r01/sweeps/onepass6_probe.jsonl,
+// onepass_variants.jsonl
+template <typename T> struct OpLU { static constexpr int LU = 4; };
+template <> struct OpLU<bf16_t> { static constexpr int LU = 2; };
+template <typename T, int V> struct OpVar;
+template <typename T> struct OpVar<T, 0> { static constexpr int NB = 16, PF = 3; };
+template <typename T> struct OpVar<T, 1> { static constexpr int NB = 18, PF = 4; };
+template <typename T> struct OpVar<T, 2> { static constexpr int NB = 14, PF = 3; };
+template <typename T> struct OpVar<T, 3> { static constexpr int NB = 17, PF = 4; };
+template <> struct OpVar<bf16_t, 0> { static constexpr int NB = 20, PF = 6; };
+template <> struct OpVar<bf16_t, 1> { static constexpr int NB = 24, PF = 4; };
+template <> struct OpVar<bf16_t, 2> { static constexpr int NB = 22, PF = 6; };
+template <> struct OpVar<bf16_t, 3> { static constexpr int NB = 18, PF = 6; };
+constexpr int kOpVariants = 4;
 
+template <typename T, int V>
+const void* onepass_fn_v() { return (const void*)k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU>; }
 template <typename T>
-const void* onepass_fn_t() { return (const void*)k_onepass<T, OpCfg<T>::NB, OpCfg<T>::PF, OpCfg<T>::LU>; }
-const void* onepass_fn(int dtype) {
-    return dtype == BPGL_F32 ? onepass_fn_t<float>() : dtype == BPGL_F64 ? onepass_fn_t<double>() : onepass_fn_t<bf16_t>();
+const void* onepass_fn_t(int v) {
+    switch (v) {
+        case 1: return onepass_fn_v<T, 1>();
+        case 2: return onepass_fn_v<T, 2>();
+        case 3: return onepass_fn_v<T, 3>();
+        default: return onepass_fn_v<T, 0>();
+    }
+}
+const void* onepass_fn(int dtype, int v) {
+    return dtype == BPGL_F32 ? onepass_fn_t<float>(v) : dtype == BPGL_F64 ? onepass_fn_t<double>(v) : onepass_fn_t<bf16_t>(v);
+}
+template <typename T, int V>
+void onepass_launch_v(bpgl_ctx* c) {
+    hipLaunchKernelGGL((k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU>),
+                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, c->p, c->op);
 }
 template <typename T>
 void onepass_launch_t(bpgl_ctx* c) {
-    hipLaunchKernelGGL((k_onepass<T, OpCfg<T>::NB, OpCfg<T>::PF, OpCfg<T>::LU>),
-                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, c->p, c->op);
+    switch (c->op_variant) {
+        case 1: onepass_launch_v<T, 1>(c); break;
+        case 2: onepass_launch_v<T, 2>(c); break;
+        case 3: onepass_launch_v<T, 3>(c); break;
+        default: onepass_launch_v<T, 0>(c); break;
+    }
 }
 int onepass_launch(bpgl_ctx* c) {
     switch (c->dtype) {
@@ -282,7 +313,15 @@ Params op_params(const bpgl_ctx* c) {
     q.slab_g = c->op.G;
     q.nchunk = 1;
     q.nseg = 1;
+    q.nparts = c->op_tail_grid;   // shrink partials come from k_onepass_tail
     return q;
+}
+template <bool UPDATE>
+int onepass_tail(bpgl_ctx* c) {
+    hipLaunchKernelGGL(k_onepass_tail<UPDATE>, dim3((unsigned)c->op_tail_grid), dim3(kThreads), 0, c->stream,
+                       op_params(c), c->op);
+    LAUNCH_CHECK("k_onepass_tail");
+    return 0;
 }
 // exact g = A^T r into G (at reset and every op_refresh iterations)
 int onepass_refresh(bpgl_ctx* c) {
@@ -291,7 +330,7 @@ int onepass_refresh(bpgl_ctx* c) {
     hipLaunchKernelGGL(k_colreduce, dim3((unsigned)cdiv(c->wp, kThreads)), dim3(kThreads), 0, c->stream, c->p.slab_g,
                        c->wp, c->nchunk, c->op.G, (double*)nullptr);
     LAUNCH_CHECK("k_colreduce");
-    return 0;
+    return onepass_tail<false>(c);   // the shrink of the next iteration from the exact g
 }
 // can this solver run use the one-pass iteration?  (0 yes; else the reason)
 const char* onepass_ineligible(bpgl_ctx* c) {
@@ -299,7 +338,7 @@ const char* onepass_ineligible(bpgl_ctx* c) {
     if (c->nranks != 1 || c->comm || c->external) return "needs a single rank without a communicator";
     if (c->fused) return "not combined with the fused iteration";
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype), kThreads, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_variant), kThreads, 0) != hipSuccess || nb < 1)
         return "kernel does not fit on a CU";
     if ((int64_t)c->op_ngroups * c->op_SB > (int64_t)nb * c->cus) return "grid exceeds the resident capacity";
     return nullptr;
@@ -370,31 +409,22 @@ int finalize_fused(bpgl_ctx* c) {
 // phase 0: colpass, shrink, rowpass, rowreduce [, allreduce, step]; phase 1: update.
 // With the caller doing the exchange (external ranks) phase 0 stops after
 // rowreduce and phase 1 starts with the step.
-// one-pass iteration: shrink (g from G), k_onepass (s23 and U partials), rowreduce of s23
-// + line search; phase 1: x / Ax update and g += gamma U
+// one-pass iteration, three kernels: k_onepass (s23 and the U partials; its row groups also
+// fold r.s23 and s23.s23), k_linesearch; phase 1: k_onepass_tail (x, Ax, r, g += gamma U and
+// the next iteration's shrink)
 int enqueue_phase_onepass(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
     if (phase == 0) {
-        const Params q = op_params(c);
-        ev_record(c, it, 1, 0);
-        hipLaunchKernelGGL(k_shrink, dim3((unsigned)c->nparts), dim3(kThreads), 0, c->stream, q);
-        LAUNCH_CHECK("k_shrink");
-        ev_record(c, it, 1, 1);
         ev_record(c, it, 7, 0);
         if ((rc = onepass_launch(c))) return rc;
         ev_record(c, it, 7, 1);
         ev_record(c, it, 3, 0);
-        if ((rc = rowreduce_p(c, q, c->op.S, c->p.comm, 1))) return rc;
+        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, op_params(c), c->op_ngroups);
+        LAUNCH_CHECK("k_linesearch");
         ev_record(c, it, 3, 1);
     } else {
         ev_record(c, it, 6, 0);
-        const int64_t nupd = std::max<int64_t>(c->wp, c->m);
-        const unsigned ublocks = (unsigned)std::min<int64_t>(cdiv(nupd, kThreads), 1024);
-        hipLaunchKernelGGL(k_update, dim3(ublocks), dim3(kThreads), 0, c->stream, c->p);
-        LAUNCH_CHECK("k_update");
-        hipLaunchKernelGGL(k_onepass_gupdate, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024)),
-                           dim3(kThreads), 0, c->stream, c->p, c->op);
-        LAUNCH_CHECK("k_onepass_gupdate");
+        if ((rc = onepass_tail<true>(c))) return rc;
         ev_record(c, it, 6, 1);
     }
     return 0;
@@ -581,7 +611,7 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     c->op = OnePassArgs{};
     if (c->op_shape) {
         c->op.G = (double*)(s + L.opG);
-        c->op.S = (double*)(s + L.opS);
+        c->op.S = p.comm;   // s23 goes straight into the exchange buffer k_update reads
         c->op.Us = (double*)(s + L.opUs);
         c->op.PG = (unsigned long long*)(s + L.opPG);
         c->op.SB = c->op_SB;
@@ -868,6 +898,13 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "onepass")) {
         if (value < -1 || value > 1) return fail(BPGL_E_ARG, "onepass must be -1, 0 or 1");
         c->onepass = (int)value;
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "onepass_variant")) {
+        if (value < 0 || value >= kOpVariants) return fail(BPGL_E_ARG, "onepass_variant must be in [0, %d)", kOpVariants);
+        c->op_variant = (int)value;
         drop_graphs(c);
         c->solver = false;
         return 0;

@@ -39,10 +39,11 @@ constexpr int kOpSlots = 1 << kOpSlotsLog;   // LDS partial slots (rows); > LAG 
 constexpr int kOpDelta = 1;     // rows between a row's phase 1 and its publication
 constexpr int kOpMaxSB = 64;    // one granule per lane
 constexpr unsigned kOpPolls = 1u << 16;
+constexpr int kOpTailBlocks = 1024;   // k_onepass_tail grid cap (= its shrink partial count)
 
 struct OnePassArgs {
     double* G;                   // [wp]   gradient carried across iterations
-    double* S;                   // [m]    s23 = A D
+    double* S;                   // [m]    s23 = A D (the solver's exchange buffer)
     double* Us;                  // [ngroups][wp] U partial of each row group
     unsigned long long* PG;      // [m][SB] tagged row partials
     int SB, ngroups, R, xl;      // segment blocks per row, row groups, rows per group, XCD-local map
@@ -80,10 +81,32 @@ __device__ __forceinline__ double op_lane(double x, int l) {
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-// wave sum in a fixed order, uniform result: 16-lane rows, then (r0 + r1) + (r2 + r3)
-__device__ __forceinline__ double op_wave_sum(double x) {
-    x = op_row_sum16(x);
-    return (op_lane(x, 0) + op_lane(x, 16)) + (op_lane(x, 32) + op_lane(x, 48));
+// x + (x of the partner 16-lane row: rows 0<->1, 2<->3), the same bits in both rows
+// (gfx950 v_permlane16_swap; VALU, no LDS round trip, no readlane)
+__device__ __forceinline__ double op_xrow16(double x) {
+    const long long b = __double_as_longlong(x);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    const double p = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);   // rows (0, 0, 2, 2)
+    const double q = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);   // rows (1, 1, 3, 3)
+    return p + q;
+}
+// x + (x of the other 32-lane half), the same bits in every lane (v_permlane32_swap)
+__device__ __forceinline__ double op_xhalf32(double x) {
+    const long long b = __double_as_longlong(x);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    const double p = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);   // lanes 0-31 in both halves
+    const double q = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);   // lanes 32-63 in both halves
+    return p + q;
+}
+// wave sum in a fixed order ((row0 + row1) + (row2 + row3)), the same bits in every lane
+__device__ __forceinline__ double op_wave_sum(double x) { return op_xhalf32(op_xrow16(op_row_sum16(x))); }
+// (lanes 0 + 1) + (lanes 2 + 3) of every quad, in every lane of the quad
+__device__ __forceinline__ double op_quad_sum(double x) {
+    x += op_dpp<0xb1>(x);
+    x += op_dpp<0x4e>(x);
+    return x;
 }
 
 template <int LU, typename T>
@@ -113,7 +136,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     const long long i0 = (long long)grp * o.R;
     const long long i1 = i0 + o.R < p.m ? i0 + o.R : p.m;
     const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
-    if (nrows == 0) return;   // the whole row group (uniform)
+    if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
+        if (sb == 0 && threadIdx.x == 0) { p.parts2[2ll * grp] = 0.0; p.parts2[2ll * grp + 1] = 0.0; }
+        return;
+    }
     const unsigned tag = (unsigned)((p.st->op_epoch + 1) & 1);   // bound scratch is zero: parity 0 = unwritten
     if (b == 0 && threadIdx.x == 0) p.st->op_ran = 1;
 
@@ -154,79 +180,97 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         gv[slot] = __hip_atomic_load(o.PG + (i0 + t2) * SB + glane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
 
+    // one row step: prefetch row t + PF (and the granules of its phase 2), phase 1 of row t,
+    // publication of row t - 1, phase 2 of row t - LAG.  (A branch-free steady-state copy of
+    // the loop made the register allocator spill: the three loop copies are not worth it.)
+    auto step = [&](const int q, const int t) {
+        const int qn = (q + PF) % NB;
+        gload(t + PF, qn);
+        load(t + PF, qn);
+        if (t < nrows) {   // phase 1: this wave's partial of s23[t] into its LDS slot
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};   // 4 independent FMA chains, folded in a fixed order
 #pragma unroll
-    for (int q = 0; q < PF; ++q) { gload(q, q); load(q, q); }
-    for (int base = 0; base < nrows + LAG; base += NB) {
+            for (int k = 0; k < LU; ++k) {
+                double v[N];
+                VecT<T>::cvt(buf[q][k], v);
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            const int t = base + q;
-            const int qn = (q + PF) % NB;
-            gload(t + PF, qn);
-            load(t + PF, qn);
-            if (t < nrows) {   // phase 1: this wave's partial of s23[t] into its LDS slot
-                double s = 0.0;
-#pragma unroll
-                for (int k = 0; k < LU; ++k) {
-                    double v[N];
-                    VecT<T>::cvt(buf[q][k], v);
-#pragma unroll
-                    for (int e = 0; e < N; ++e) s = fma(v[e], d[k][e], s);
-                }
-                s = op_wave_sum(s);
-                if (lane == 0)
-                    __hip_atomic_store(&part[t % kOpSlots][wave], op_stuff(s, (unsigned)t >> kOpSlotsLog),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int e = 0; e < N; ++e) acc[(k * N + e) & 3] = fma(v[e], d[k][e], acc[(k * N + e) & 3]);
             }
-            const int tp = t - kOpDelta;   // publication of row tp by wave tp % 4
-            if (tp >= 0 && tp < nrows && (tp & 3) == wave) {
-                const unsigned want = ((unsigned)tp >> kOpSlotsLog) & 1u;
-                op_u64 w = 0;
-                while (true) {
-                    w = lane < kWaves ? __hip_atomic_load(&part[tp % kOpSlots][lane], __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_WORKGROUP)
-                                      : 0;
-                    if (__all(lane >= kWaves || op_tag(w) == want)) break;
+            const double s = op_wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+            if (lane == 0)
+                __hip_atomic_store(&part[t % kOpSlots][wave], op_stuff(s, (unsigned)t >> kOpSlotsLog),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        const int tp = t - kOpDelta;   // publication of row tp by wave tp % 4
+        if (tp >= 0 && tp < nrows && (tp & 3) == wave) {
+            const unsigned want = ((unsigned)tp >> kOpSlotsLog) & 1u;
+            op_u64 w = 0;
+            while (true) {
+                w = lane < kWaves ? __hip_atomic_load(&part[tp % kOpSlots][lane], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP)
+                                  : 0;
+                if (__all(lane >= kWaves || op_tag(w) == want)) break;
+                if (polls == 0) { failed = true; break; }
+                --polls;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            const double bsum = op_quad_sum(op_unstuff(w));   // (p0 + p1) + (p2 + p3) in lane 0
+            if (lane == 0)
+                __hip_atomic_store(o.PG + (i0 + tp) * SB + sb, op_stuff(bsum, tag), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const int t2 = t - LAG;
+        if (t2 >= 0 && t2 < nrows) {   // phase 2: U += row(t2) * s23[t2]
+            const int qs = (q - LAG + NB) % NB;
+            op_u64 v = gv[q];
+            auto ready = [&](op_u64 g) { return lane >= SB || op_tag(g) == tag; };
+            if (!__all(ready(v))) {   // late: re-poll (drains this wave's queue; rare)
+                const op_u64* src = o.PG + (i0 + t2) * SB + glane;
+                do {
                     if (polls == 0) { failed = true; break; }
                     --polls;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                const double x = op_unstuff(w);
-                const double bsum = (op_lane(x, 0) + op_lane(x, 1)) + (op_lane(x, 2) + op_lane(x, 3));
-                if (lane == 0)
-                    __hip_atomic_store(o.PG + (i0 + tp) * SB + sb, op_stuff(bsum, tag), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_s_sleep(2);
+                    v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } while (!__all(ready(v)));
+                // settle here, so the merge with the fast path is not a pending load
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                asm volatile("" : "+v"(v));
             }
-            const int t2 = t - LAG;
-            if (t2 >= 0 && t2 < nrows) {   // phase 2: U += row(t2) * s23[t2]
-                const int qs = (q - LAG + NB) % NB;
-                op_u64 v = gv[q];
-                auto ready = [&](op_u64 g) { return lane >= SB || op_tag(g) == tag; };
-                if (!__all(ready(v))) {   // late: re-poll (drains this wave's queue; rare)
-                    const op_u64* src = o.PG + (i0 + t2) * SB + glane;
-                    do {
-                        if (polls == 0) { failed = true; break; }
-                        --polls;
-                        __builtin_amdgcn_s_sleep(2);
-                        v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    } while (!__all(ready(v)));
-                    // settle here, so the merge with the fast path is not a pending load
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    asm volatile("" : "+v"(v));
-                }
-                double x = lane < SB ? op_unstuff(v) : 0.0;
-                x = SB <= 16 ? op_lane(op_row_sum16(x), 0) : op_wave_sum(x);
-                if (sb == 0 && wave == 0 && lane == 0) o.S[i0 + t2] = x;
+            double x = lane < SB ? op_unstuff(v) : 0.0;
+            x = SB <= 16 ? op_lane(op_row_sum16(x), 0) : op_wave_sum(x);
+            if (sb == 0 && wave == 0 && lane == 0) o.S[i0 + t2] = x;
 #pragma unroll
-                for (int k = 0; k < LU; ++k) {
-                    double v2[N];
-                    VecT<T>::cvt(buf[qs][k], v2);
+            for (int k = 0; k < LU; ++k) {
+                double v2[N];
+                VecT<T>::cvt(buf[qs][k], v2);
 #pragma unroll
-                    for (int e = 0; e < N; ++e) u[k][e] = fma(v2[e], x, u[k][e]);
-                }
+                for (int e = 0; e < N; ++e) u[k][e] = fma(v2[e], x, u[k][e]);
             }
         }
+    };
+
+#pragma unroll
+    for (int q = 0; q < PF; ++q) { gload(q, q); load(q, q); }
+    for (int base = 0; base < nrows + LAG; base += NB) {   // base stays a multiple of NB: slots are static
+#pragma unroll
+        for (int q = 0; q < NB; ++q) step(q, base + q);
     }
     if (failed && lane == 0) atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
+    if (sb == 0 && wave == 0) {
+        // this row group's share of the line search, r.s23 and s23.s23, from the s23 rows this
+        // wave wrote (fixed order: lanes stride the rows, then the wave sum) -> parts2[grp]
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __threadfence_block();
+        double rs = 0.0, ss = 0.0;
+        for (int i = lane; i < nrows; i += 64) {
+            const double sv = o.S[i0 + i];
+            rs = fma(p.r[i0 + i], sv, rs);
+            ss = fma(sv, sv, ss);
+        }
+        rs = op_wave_sum(rs);
+        ss = op_wave_sum(ss);
+        if (lane == 0) { p.parts2[2ll * grp] = rs; p.parts2[2ll * grp + 1] = ss; }
+    }
     double* dst = o.Us + (long long)grp * p.wp;
 #pragma unroll
     for (int k = 0; k < LU; ++k)
@@ -235,19 +279,78 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
 }
 
-// g += gamma * sum_groups Us (fixed order) after the line search; advances the launch
-// parity iff k_onepass ran (it also runs in the iteration whose line search stops)
-__global__ __launch_bounds__(kThreads) void k_onepass_gupdate(Params p, OnePassArgs o) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && p.st->op_ran) {
+// Tail of a one-pass iteration, one kernel.  UPDATE: x += gamma D, Ax += gamma s23,
+// r = Ax - b (lasso.py:153-155, :105), g += gamma sum_groups U (fixed order); then, for every
+// mode, the shrink of the next iteration from (g, x) (lasso.py:114-119, cpu_calculation.py:
+// 15-20): D, g mirrored to p.g, and per-block [sum|Bx|, sum|x|, max err] partials that
+// k_linesearch folds (p.nparts = gridDim.x).  UPDATE = false runs the shrink alone (after a
+// reset or an exact refresh of g).  UPDATE also advances the launch parity iff k_onepass ran
+// (it runs in the iteration whose line search stops, too).
+template <bool UPDATE>
+__global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs o) {
+    if (UPDATE && blockIdx.x == 0 && threadIdx.x == 0 && p.st->op_ran) {
         p.st->op_epoch += 1;
         p.st->op_ran = 0;
     }
     if (p.st->done) return;
-    const double gamma = p.st->gamma;
-    for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < p.wp; j += (long long)gridDim.x * kThreads) {
-        double acc = 0.0;
-        for (int g = 0; g < o.ngroups; ++g) acc += o.Us[(long long)g * p.wp + j];
-        o.G[j] += gamma * acc;
+    const double gamma = UPDATE ? p.st->gamma : 0.0;
+    const long long stride = (long long)gridDim.x * kThreads;
+    const long long k0 = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (UPDATE) {
+        for (long long k = k0; k < p.m; k += stride) {
+            const double ax = p.Ax[k] + gamma * o.S[k];
+            p.Ax[k] = ax;
+            p.r[k] = ax - p.b[k];
+        }
+    }
+    double abx = 0.0, ax1 = 0.0, err = 0.0;
+    for (long long j = k0; j < p.wp; j += stride) {
+        double g = o.G[j];
+        if (UPDATE) {
+            double acc = 0.0;
+            for (int q = 0; q < o.ngroups; ++q) acc += o.Us[(long long)q * p.wp + j];
+            g += gamma * acc;
+            o.G[j] = g;
+        }
+        p.g[j] = g;
+        double Dj = 0.0;
+        if (j < p.w) {
+            double xj = p.x[j];
+            if (UPDATE) {
+                xj += gamma * p.D[j];
+                p.x[j] = xj;
+            }
+            const double rx = p.diag[j] * xj - g;                 // lasso.py:114
+            const double bx = p.rec[j] * soft_thr(rx, p.mu);      // lasso.py:115-117
+            Dj = bx - xj;                                         // lasso.py:119
+            abx += fabs(bx);
+            ax1 += fabs(xj);
+            const double e = fabs(g - proj(g - xj, -p.mu, p.mu)); // cpu_calculation.py:15-20
+            err = (e > err || e != e) ? e : err;
+        }
+        p.D[j] = Dj;
+    }
+    abx = wave_sum(abx);
+    ax1 = wave_sum(ax1);
+    err = wave_max(err);
+    __shared__ double red[3][kWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { red[0][wave] = abx; red[1][wave] = ax1; red[2][wave] = err; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double e = red[2][0];
+        for (int q = 1; q < kWaves; ++q) e = (red[2][q] > e || red[2][q] != red[2][q]) ? red[2][q] : e;
+        double* dst = p.parts + 4ll * blockIdx.x;
+        dst[0] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        dst[1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+        dst[2] = e;
+        dst[3] = 0.0;
+        if (UPDATE && blockIdx.x == 0) {
+            const long long t = p.st->t - 1;
+            p.st->iters = t + 1;
+            if (p.time_iter && t < p.rec_len)
+                p.time_iter[t + 1] = (double)(wall_clock64() - p.st->t_base) * p.wall_tick_s;
+        }
     }
 }
 
