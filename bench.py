@@ -7,13 +7,18 @@ A D, the line search and the update -- all on the device, inputs resident in
 HBM before the timed region.
 
   N = 1 : BASELINE configs[1]  m=8192 n=65536 fp32 A, one feature block.
-  N > 1 : BASELINE configs[2]  m=8192 n=65536*N, every GPU holds an 8192 x 65536
-          column shard (weak scaling; the per-GPU work of N = 1), one RCCL
-          all-reduce of m + 2 + N fp64 values per iteration.  The work unit is
-          one "block-iteration" = one iteration over an 8192 x 65536 fp32 block
-          (4.30e9 algorithmic bytes), so value = N x global iterations/s.
+  N > 1 : BASELINE configs[2]  m=8192 n=65536*N (n = 524288 at N = 8), weak scaling:
+          every GPU holds 2 GiB of A, the per-GPU work of N = 1.  Default
+          (--shard rows): GPU g holds rows [g m/N, (g+1) m/N) of A (all columns),
+          streams them once per iteration (k_onepass), and ONE RCCL all-reduce of
+          n + 2 fp64 values per iteration carries U = A^T A D and the line-search
+          dot products.  --shard columns: the reference's column split (every GPU
+          an 8192 x 65536 column shard), two passes over A per iteration and one
+          all-reduce of m + 2 + N fp64 (the residual side).  The work unit is one
+          "block-iteration" = one iteration's worth of an 8192 x 65536 fp32 matrix
+          (the whole configs[1] matrix), so value = N x global iterations/s.
           A strong-scaling measurement (the fixed 8192 x 65536 matrix split
-          N ways) is reported beside it under "strong".
+          N ways the same way) is reported beside it under "strong".
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
@@ -84,6 +89,9 @@ def parse():
     ap.add_argument("--onepass-variant", type=int, default=0, help="one-pass ring depth / prefetch variant (0-3)")
     ap.add_argument("--comm", action="store_true",
                     help="attach an RCCL communicator even at N = 1 (runs the sharded/all-reduce leg)")
+    ap.add_argument("--shard", default="rows", choices=["rows", "columns"],
+                    help="multi-GPU split (N > 1, or N = 1 with --comm): rows (default; one pass over A, "
+                         "all-reduce of n + 2) or columns (the reference's split; two passes, all-reduce of m + 2 + N)")
     ap.add_argument("--rhs", type=int, default=1,
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
@@ -123,18 +131,20 @@ class Ctx:
         return float(t[0])
 
 
-def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False):
+def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, shard="rows"):
     import torch
-    from convex_optimization_amd.distributed import RankComm, shard_bounds
+    from convex_optimization_amd.distributed import RankComm, row_bounds, shard_bounds
     from convex_optimization_amd.parameters import device_instance
     comm = RankComm(ctx.rank, ctx.world) if (ctx.world > 1 or force_comm) else None
-    col_range = None
-    if ctx.world > 1:
+    col_range = row_range = None
+    if comm is not None and shard == "rows":
+        row_range = row_bounds(m, ctx.rank, ctx.world)
+    elif ctx.world > 1:
         bounds = shard_bounds(n_total, block, ctx.rank, ctx.world)
         idx = torch.cat([torch.arange(s, e) for s, e in bounds]).to(f"cuda:{ctx.local}")
         col_range = idx
     gc, b, mu, _ = device_instance(m, n_total, 0.4, block, TYPE=type_name, seed=seed, device=ctx.local,
-                                   comm=comm, col_range=col_range)
+                                   comm=comm, col_range=col_range, row_range=row_range)
     torch.cuda.synchronize()
     return gc, b, mu
 
@@ -156,7 +166,7 @@ def timed_window(ctx, gc, steps, graph):
 
 
 def measure(ctx, args, m, n_total):
-    gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm)
+    gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard)
     gc.set_tuning("fused", args.fused)
     gc.set_tuning("onepass", args.onepass)
     gc.set_tuning("onepass_variant", args.onepass_variant)
@@ -174,7 +184,7 @@ def measure(ctx, args, m, n_total):
     times, samples = gc.kernel_times()
     gc.set_kernel_timing(False)
     return dict(gc=gc, el_graph=el_graph, el_events=el_ev, kernel_ms=times, samples=samples, status=st,
-                w_local=gc.MAT_WIDTH, b=b, mu=mu)
+                w_local=gc.MAT_WIDTH, m_local=gc.MAT_HEIGHT, b=b, mu=mu)
 
 
 def cpu_baseline(gc, b, mu, seconds):
@@ -358,11 +368,30 @@ def main_panel(args):
                      "frac": tflops / MFMA_BF16_DENSE_TFLOPS, "flops_per_launch": flops},
         },
     }
-    print(json.dumps(out))
+    emit(out)
+
+
+_JSON_OUT = None
+
+
+def quiet_stdout():
+    """Route fd 1 to stderr for the rest of the run (RCCL prints its version banner on
+    stdout at communicator init); the JSON line goes to the original stdout via emit()."""
+    global _JSON_OUT
+    if _JSON_OUT is None:
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
+def emit(out):
+    (_JSON_OUT or sys.stdout).write(json.dumps(out) + "\n")
+    (_JSON_OUT or sys.stdout).flush()
 
 
 def main():
     args = parse()
+    quiet_stdout()
     if args.rhs > 1:
         return main_panel(args)
     import torch
@@ -371,15 +400,16 @@ def main():
     m = args.m
     n_total = args.n_per_gpu * G
     res = measure(ctx, args, m, n_total)
-    w = res["w_local"]
+    w, ml = res["w_local"], res["m_local"]
+    rows = res["gc"].shard == "rows"
     iters_s_graph = args.steps / res["el_graph"]
     iters_s_ev = args.steps / res["el_events"]
     kms = res["kernel_ms"]
     sa = {"float": 4, "double": 8, "bf16": 2}[args.type]
     onepass = kms.get("onepass", 0.0) > 0
     if onepass:
-        dom, dom_bytes, kname = "onepass", alg_bytes_onepass(m, w, sa), "k_onepass"
-        it_bytes = alg_bytes_iter_onepass(m, w, sa)
+        dom, dom_bytes, kname = "onepass", alg_bytes_onepass(ml, w, sa), "k_onepass"
+        it_bytes = alg_bytes_iter_onepass(ml, w, sa)
     else:
         dom = max(("colpass", "rowpass"), key=lambda k: kms[k])
         dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(m, w, sa)
@@ -387,12 +417,13 @@ def main():
                  ("colpass", 0): "k_colpass", ("rowpass", 0): "k_rowpass"}[(dom, int(args.fused))]
         it_bytes = alg_bytes_iter(m, w, sa)
     achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
-    workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}"
+    workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}" + ("_rows" if rows and G > 1 else "")
     traffic = pmc_traffic(workload_key, kname)
     out = {
         "metric": METRIC,
         "value": iters_s_graph * G,
-        "unit": "block-iters/s (1 block-iter = 1 iteration over an 8192x65536 fp32 column block)"
+        "unit": "block-iters/s (1 block-iter = one iteration's worth of an 8192x65536 fp32 matrix, "
+                "the per-GPU share; = N x global iterations/s)"
         if G > 1 else "iters/s",
         "n_gpus": G,
         "steps": args.steps,
@@ -405,19 +436,24 @@ def main():
         "data": "synthetic (A ~ N(0,1) rows unit-norm, generated in HBM; x_true density 0.4; b = A x_true + 0.01 e)",
         "config": {
             "workload": ("configs[1]: m=8192 n=65536 fp32 A, 1 feature block, 1 GPU" if G == 1 else
+                         f"configs[2]-style: m={m} n={n_total} fp32 A, 1 feature block, row-sharded "
+                         f"{ml} rows/GPU x {G} GPUs, one RCCL all-reduce of n+2 fp64 per iteration" if rows else
                          f"configs[2]-style: m={m} n={n_total} fp32 A, 1 feature block, column-sharded "
-                         f"{w} cols/GPU x {G} GPUs, RCCL all-reduce per iteration"),
-            "m": m, "n": n_total, "n_local": w, "feature_blocks": args.block, "a_storage": args.type,
-            "accumulate": "fp64", "parallelism": f"column-shard x{G}", "rccl": bool(G > 1 or args.comm),
+                         f"{w} cols/GPU x {G} GPUs, RCCL all-reduce of m+2+N fp64 per iteration"),
+            "m": m, "n": n_total, "m_local": ml, "n_local": w, "feature_blocks": args.block,
+            "a_storage": args.type, "accumulate": "fp64",
+            "parallelism": f"{'row' if rows else 'column'}-shard x{G}", "rccl": bool(G > 1 or args.comm),
             "global_iters_per_s": iters_s_graph,
             "iteration": ("one pass over A (k_onepass: s23 = A D and U = A^T s23 together; g += gamma U, "
-                          "exact g = A^T r every 64 iterations)" if onepass else
+                          "exact g = A^T r every 64 iterations)" + (
+                              "; row shards: k_onepass_fold + RCCL all-reduce of [U | r.s23 | s23.s23]"
+                              if rows and G > 1 else "") if onepass else
                           "two passes over A (A^T r, then A D)"),
             "alg_bytes_per_iter_per_gpu": it_bytes,
             "hbm_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / it_bytes,
             "iter_roofline_frac": iters_s_graph * it_bytes / (HBM_PEAK_GBS * 1e9),
-            "two_pass_alg_bytes_per_iter_per_gpu": alg_bytes_iter(m, w, sa),
-            "two_pass_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(m, w, sa),
+            "two_pass_alg_bytes_per_iter_per_gpu": alg_bytes_iter(ml, w, sa),
+            "two_pass_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(ml, w, sa),
             "launch_mode": "hipGraph replay of one iteration (value); eager + HIP events (kernel times)", "fused": args.fused,
             "iters_per_s_eager_with_events": iters_s_ev,
             "kernel_avg_ms": kms,
@@ -442,7 +478,8 @@ def main():
         a2 = argparse.Namespace(**vars(args))
         strong = measure(ctx, a2, m, args.n_per_gpu)
         out["strong"] = {"value": args.steps / strong["el_graph"], "unit": "iters/s",
-                         "config": f"m={m} n={args.n_per_gpu} split {G} ways ({strong['w_local']} cols/GPU)",
+                         "config": f"m={m} n={args.n_per_gpu} split {G} ways ({strong['m_local']} rows x "
+                                   f"{strong['w_local']} cols per GPU)",
                          "kernel_avg_ms": strong["kernel_ms"]}
         res = strong
     if G == 1 and args.type == "float":
@@ -451,7 +488,7 @@ def main():
     if G == 1 and ctx.rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds)
     if ctx.rank == 0:
-        print(json.dumps(out))
+        emit(out)
     if ctx.world > 1:
         ctx.dist.destroy_process_group()
 

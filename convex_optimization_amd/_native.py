@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(_HERE, "_lib", "libbpgl.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bpgl.h")
 
 BPGL_F32, BPGL_F64, BPGL_BF16 = 0, 1, 2
+BPGL_SHARD_COLUMNS, BPGL_SHARD_ROWS = 0, 1
 _DTYPES = {
     "float": BPGL_F32, "float32": BPGL_F32, "f32": BPGL_F32,
     "double": BPGL_F64, "float64": BPGL_F64, "f64": BPGL_F64,
@@ -44,6 +45,8 @@ _SIGS = {
     "bpgl_block_width_padded": (_i64, [_p]),
     "bpgl_bind": (_int, [_p, _p, _i64, _i64, _p, _i64]),
     "bpgl_diag_ata": (_int, [_p, _p]),
+    "bpgl_set_diag": (_int, [_p, _p]),
+    "bpgl_set_shard": (_int, [_p, _int]),
     "bpgl_mtv": (_int, [_p, _i32, _p, _p]),
     "bpgl_mv": (_int, [_p, _i32, _p, _p]),
     "bpgl_comm_unique_id": (_int, [_p]),

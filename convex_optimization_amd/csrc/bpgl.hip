@@ -86,7 +86,11 @@ struct bpgl_ctx {
     int op_variant = 0;        // ring depth / prefetch variant (OpVar)
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
-    int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0;
+    int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
+    // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
+    // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
+    bool rows = false;
+    bool op_refresh_pending = false;   // external rows: phase 2 ran, phase 3 not yet
     int64_t op_t = 0;          // iterations enqueued since the solver reset
     OnePassArgs op{};
 };
@@ -119,6 +123,7 @@ void geometry(bpgl_ctx* c) {
                  : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<2, bf16_t>::BC;
     const int64_t SB = cdiv(c->wp, bc);
     c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
+    c->op_gpl = SB > 64 ? 2 : 1;
     if (c->op_shape) {
         int64_t ng = std::min<int64_t>(c->cus / SB, c->m);
         const int64_t R = cdiv(c->m, ng);
@@ -135,7 +140,7 @@ void geometry(bpgl_ctx* c) {
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opUs, opPG, total;
+    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opUs, opPG, opS, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -149,7 +154,8 @@ Layout layout(const bpgl_ctx* c) {
     L.parts2 = k.take(8 * 2 * std::max<int64_t>(kMaxReduceBlocks, c->nchunk));
     L.Dbuf = k.take(8 * 2 * c->wp);
     L.cnt = k.take(8 * ((int64_t)c->nseg + c->nchunk));
-    L.comm = k.take(8 * (c->m + 2 + kMaxRanks));
+    // column shards exchange [s23 (m) | 2 | err slots]; row shards [U (wp) | r.s23 | s23.s23]
+    L.comm = k.take(8 * std::max<int64_t>(c->m + 2 + kMaxRanks, c->wp + 2));
     L.r = k.take(8 * c->m);
     L.Ax = k.take(8 * (int64_t)c->nblock * c->m);
     L.diag = k.take(8 * (int64_t)c->nblock * c->wp);
@@ -158,6 +164,7 @@ Layout layout(const bpgl_ctx* c) {
     L.opG = k.take(op ? 8 * c->wp : 0);
     L.opUs = k.take(op ? 8 * (int64_t)c->op_ngroups * c->wp : 0);
     L.opPG = k.take(op ? 8 * c->m * c->op_SB : 0);
+    L.opS = k.take(op && c->rows ? 8 * c->m : 0);
     L.total = k.off;
     return L;
 }
@@ -270,33 +277,42 @@ template <> struct OpVar<bf16_t, 2> { static constexpr int NB = 22, PF = 6; };
 template <> struct OpVar<bf16_t, 3> { static constexpr int NB = 18, PF = 6; };
 constexpr int kOpVariants = 4;
 
-template <typename T, int V>
-const void* onepass_fn_v() { return (const void*)k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU>; }
-template <typename T>
-const void* onepass_fn_t(int v) {
+// GPL: granules per lane of the row hand-off (SB <= 64: 1, SB <= 128: 2)
+template <typename T, int V, int GPL>
+const void* onepass_fn_v() { return (const void*)k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU, GPL>; }
+template <typename T, int GPL>
+const void* onepass_fn_g(int v) {
     switch (v) {
-        case 1: return onepass_fn_v<T, 1>();
-        case 2: return onepass_fn_v<T, 2>();
-        case 3: return onepass_fn_v<T, 3>();
-        default: return onepass_fn_v<T, 0>();
+        case 1: return onepass_fn_v<T, 1, GPL>();
+        case 2: return onepass_fn_v<T, 2, GPL>();
+        case 3: return onepass_fn_v<T, 3, GPL>();
+        default: return onepass_fn_v<T, 0, GPL>();
     }
 }
-const void* onepass_fn(int dtype, int v) {
-    return dtype == BPGL_F32 ? onepass_fn_t<float>(v) : dtype == BPGL_F64 ? onepass_fn_t<double>(v) : onepass_fn_t<bf16_t>(v);
+template <typename T>
+const void* onepass_fn_t(int v, int gpl) { return gpl == 2 ? onepass_fn_g<T, 2>(v) : onepass_fn_g<T, 1>(v); }
+const void* onepass_fn(int dtype, int v, int gpl) {
+    return dtype == BPGL_F32 ? onepass_fn_t<float>(v, gpl)
+         : dtype == BPGL_F64 ? onepass_fn_t<double>(v, gpl) : onepass_fn_t<bf16_t>(v, gpl);
 }
-template <typename T, int V>
+template <typename T, int V, int GPL>
 void onepass_launch_v(bpgl_ctx* c) {
-    hipLaunchKernelGGL((k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU>),
+    hipLaunchKernelGGL((k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU, GPL>),
                        dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, c->p, c->op);
+}
+template <typename T, int GPL>
+void onepass_launch_g(bpgl_ctx* c) {
+    switch (c->op_variant) {
+        case 1: onepass_launch_v<T, 1, GPL>(c); break;
+        case 2: onepass_launch_v<T, 2, GPL>(c); break;
+        case 3: onepass_launch_v<T, 3, GPL>(c); break;
+        default: onepass_launch_v<T, 0, GPL>(c); break;
+    }
 }
 template <typename T>
 void onepass_launch_t(bpgl_ctx* c) {
-    switch (c->op_variant) {
-        case 1: onepass_launch_v<T, 1>(c); break;
-        case 2: onepass_launch_v<T, 2>(c); break;
-        case 3: onepass_launch_v<T, 3>(c); break;
-        default: onepass_launch_v<T, 0>(c); break;
-    }
+    if (c->op_gpl == 2) onepass_launch_g<T, 2>(c);
+    else onepass_launch_g<T, 1>(c);
 }
 int onepass_launch(bpgl_ctx* c) {
     switch (c->dtype) {
@@ -316,29 +332,52 @@ Params op_params(const bpgl_ctx* c) {
     q.nparts = c->op_tail_grid;   // shrink partials come from k_onepass_tail
     return q;
 }
+// the one-pass tail's view of U: the row-group partials (one rank), or the all-reduced sum
+// in the exchange buffer (row shards)
+OnePassArgs op_tail_args(const bpgl_ctx* c) {
+    OnePassArgs o = c->op;
+    if (c->rows) {
+        o.Us = c->p.comm;
+        o.ngroups = 1;
+    }
+    return o;
+}
 template <bool UPDATE>
 int onepass_tail(bpgl_ctx* c) {
     hipLaunchKernelGGL(k_onepass_tail<UPDATE>, dim3((unsigned)c->op_tail_grid), dim3(kThreads), 0, c->stream,
-                       op_params(c), c->op);
+                       op_params(c), op_tail_args(c));
     LAUNCH_CHECK("k_onepass_tail");
     return 0;
 }
-// exact g = A^T r into G (at reset and every op_refresh iterations)
-int onepass_refresh(bpgl_ctx* c) {
+int allreduce_sum(bpgl_ctx* c, double* buf, int64_t count) {
+    ncclResult_t nr = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, c->comm, c->stream);
+    if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
+    return 0;
+}
+// this rank's A^T r into dst (row shards: a partial over ranks)
+int onepass_local_gradient(bpgl_ctx* c, double* dst) {
     int rc;
     if ((rc = colpass(c, 0, c->p.r, c->p.slab_g, -1))) return rc;
     hipLaunchKernelGGL(k_colreduce, dim3((unsigned)cdiv(c->wp, kThreads)), dim3(kThreads), 0, c->stream, c->p.slab_g,
-                       c->wp, c->nchunk, c->op.G, (double*)nullptr);
+                       c->wp, c->nchunk, dst, (double*)nullptr);
     LAUNCH_CHECK("k_colreduce");
+    return 0;
+}
+// exact g = A^T r into G (at reset and every op_refresh iterations); row shards sum it over ranks
+int onepass_refresh(bpgl_ctx* c) {
+    int rc;
+    if ((rc = onepass_local_gradient(c, c->op.G))) return rc;
+    if (c->rows && c->comm && (rc = allreduce_sum(c, c->op.G, c->wp))) return rc;
     return onepass_tail<false>(c);   // the shrink of the next iteration from the exact g
 }
 // can this solver run use the one-pass iteration?  (0 yes; else the reason)
 const char* onepass_ineligible(bpgl_ctx* c) {
-    if (!c->op_shape) return "needs one feature block and at most 64 segment blocks per row";
-    if (c->nranks != 1 || c->comm || c->external) return "needs a single rank without a communicator";
+    if (!c->op_shape) return "needs one feature block and at most 128 segment blocks per row";
+    if (!c->rows && (c->nranks != 1 || c->comm || c->external))
+        return "column shards need a single rank without a communicator (row shards run it on several)";
     if (c->fused) return "not combined with the fused iteration";
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_variant), kThreads, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_variant, c->op_gpl), kThreads, 0) != hipSuccess || nb < 1)
         return "kernel does not fit on a CU";
     if ((int64_t)c->op_ngroups * c->op_SB > (int64_t)nb * c->cus) return "grid exceeds the resident capacity";
     return nullptr;
@@ -412,8 +451,46 @@ int finalize_fused(bpgl_ctx* c) {
 // one-pass iteration, three kernels: k_onepass (s23 and the U partials; its row groups also
 // fold r.s23 and s23.s23), k_linesearch; phase 1: k_onepass_tail (x, Ax, r, g += gamma U and
 // the next iteration's shrink)
+//
+// Row shards: k_onepass, k_onepass_fold -> exchange buffer, all-reduce (RCCL), k_linesearch on
+// the summed scalars; phase 1: k_onepass_tail with the summed U.  With the exchange done by the
+// caller (external ranks) phase 0 ends after the fold and phase 1 starts with the line search.
+int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
+    int rc;
+    Params ls = op_params(c);
+    ls.parts2 = c->p.comm + c->wp;   // [r.s23, s23.s23] summed over ranks
+    if (phase == 0) {
+        ev_record(c, it, 7, 0);
+        if ((rc = onepass_launch(c))) return rc;
+        ev_record(c, it, 7, 1);
+        ev_record(c, it, 3, 0);
+        hipLaunchKernelGGL(k_onepass_fold, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024)),
+                           dim3(kThreads), 0, c->stream, c->p, c->op, c->p.comm);
+        LAUNCH_CHECK("k_onepass_fold");
+        ev_record(c, it, 3, 1);
+        if (c->comm) {
+            ev_record(c, it, 4, 0);
+            if ((rc = allreduce_sum(c, c->p.comm, c->wp + 2))) return rc;
+            ev_record(c, it, 4, 1);
+        }
+    }
+    if ((phase == 0 && !c->external) || (phase == 1 && c->external)) {
+        ev_record(c, it, 5, 0);
+        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, ls, 1);
+        LAUNCH_CHECK("k_linesearch");
+        ev_record(c, it, 5, 1);
+    }
+    if (phase == 1) {
+        ev_record(c, it, 6, 0);
+        if ((rc = onepass_tail<true>(c))) return rc;
+        ev_record(c, it, 6, 1);
+    }
+    return 0;
+}
+
 int enqueue_phase_onepass(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
+    if (c->rows) return enqueue_phase_onepass_rows(c, it, phase);
     if (phase == 0) {
         ev_record(c, it, 7, 0);
         if ((rc = onepass_launch(c))) return rc;
@@ -611,7 +688,9 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     c->op = OnePassArgs{};
     if (c->op_shape) {
         c->op.G = (double*)(s + L.opG);
-        c->op.S = p.comm;   // s23 goes straight into the exchange buffer k_update reads
+        // s23 goes straight into the exchange buffer k_update reads (row shards: that buffer
+        // carries U, s23 stays local)
+        c->op.S = c->rows ? (double*)(s + L.opS) : p.comm;
         c->op.Us = (double*)(s + L.opUs);
         c->op.PG = (unsigned long long*)(s + L.opPG);
         c->op.SB = c->op_SB;
@@ -646,9 +725,42 @@ int bpgl_diag_ata(bpgl_ctx* c, double* out) {
                            c->p.slab_g, c->wp, c->nchunk, dst, rdst);
         LAUNCH_CHECK("k_colreduce");
     }
+    if (c->rows && c->comm) {   // row shards: column norms are sums over ranks
+        double* dg = const_cast<double*>(c->p.diag);
+        if ((rc = allreduce_sum(c, dg, c->wp))) return rc;
+        hipLaunchKernelGGL(k_recip, dim3((unsigned)cdiv(c->wp, kThreads)), dim3(kThreads), 0, c->stream, dg,
+                           const_cast<double*>(c->p.rec), c->wp);
+        LAUNCH_CHECK("k_recip");
+    }
     if (out)
         HIP_TRY(hipMemcpyAsync(out, c->p.diag, 8 * (size_t)c->nblock * c->wp, hipMemcpyDeviceToDevice, c->stream));
     c->have_diag = true;
+    return 0;
+}
+
+int bpgl_set_diag(bpgl_ctx* c, const double* diag) {
+    int rc;
+    if ((rc = check_ready(c))) return rc;
+    if (!diag) return fail(BPGL_E_ARG, "null diag");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t n = (int64_t)c->nblock * c->wp;
+    double* dg = const_cast<double*>(c->p.diag);
+    if (diag != dg) HIP_TRY(hipMemcpyAsync(dg, diag, 8 * (size_t)n, hipMemcpyDeviceToDevice, c->stream));
+    hipLaunchKernelGGL(k_recip, dim3((unsigned)cdiv(n, kThreads)), dim3(kThreads), 0, c->stream, dg,
+                       const_cast<double*>(c->p.rec), n);
+    LAUNCH_CHECK("k_recip");
+    c->have_diag = true;
+    c->solver = false;
+    drop_graphs(c);
+    return 0;
+}
+
+int bpgl_set_shard(bpgl_ctx* c, int mode) {
+    if (!c) return fail(BPGL_E_ARG, "null context");
+    if (mode != BPGL_SHARD_COLUMNS && mode != BPGL_SHARD_ROWS) return fail(BPGL_E_ARG, "unknown shard mode %d", mode);
+    if (c->bound) return fail(BPGL_E_STATE, "bpgl_set_shard must precede bpgl_bind");
+    if (mode == BPGL_SHARD_ROWS && c->nblock != 1) return fail(BPGL_E_ARG, "row shards need one feature block");
+    c->rows = mode == BPGL_SHARD_ROWS;
     return 0;
 }
 
@@ -727,8 +839,22 @@ int bpgl_solver_phase(bpgl_ctx* c, int phase) {
     int rc;
     if ((rc = check_ready(c))) return rc;
     if (!c->solver) return fail(BPGL_E_STATE, "bpgl_solver_reset has not been called");
-    if (phase != 0 && phase != 1) return fail(BPGL_E_ARG, "phase must be 0 or 1");
+    if (phase < 0 || phase > 3) return fail(BPGL_E_ARG, "phase must be 0, 1, 2 or 3");
     HIP_TRY(hipSetDevice(c->device));
+    if (phase >= 2) {   // exact-gradient exchange of external row shards
+        if (!(c->rows && c->external && c->op_on))
+            return fail(BPGL_E_STATE, "phases 2 and 3 exist for external row shards only");
+        if (phase == 2) {
+            if ((rc = onepass_local_gradient(c, c->p.comm))) return rc;
+            HIP_TRY(hipMemsetAsync(c->p.comm + c->wp, 0, 16, c->stream));
+            c->op_refresh_pending = true;
+            return 0;
+        }
+        if (!c->op_refresh_pending) return fail(BPGL_E_STATE, "phase 3 needs phase 2 first");
+        HIP_TRY(hipMemcpyAsync(c->op.G, c->p.comm, 8 * c->wp, hipMemcpyDeviceToDevice, c->stream));
+        c->op_refresh_pending = false;
+        return onepass_tail<false>(c);
+    }
     if ((rc = enqueue_phase(c, 0, phase))) return rc;
     if (phase == 1) return finalize_fused(c);
     return 0;
@@ -736,7 +862,7 @@ int bpgl_solver_phase(bpgl_ctx* c, int phase) {
 
 double* bpgl_solver_exchange_buffer(bpgl_ctx* c, int64_t* count) {
     if (!c) return nullptr;
-    if (count) *count = c->m + 2 + c->nranks;
+    if (count) *count = c->rows ? c->wp + 2 : c->m + 2 + c->nranks;
     return c->p.comm;
 }
 
@@ -765,8 +891,8 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
         if ((rc = rowpass(c, x + (int64_t)k * c->wp, p.slab_s, k))) return rc;
         if ((rc = rowreduce(c, p.slab_s, p.Ax + (int64_t)k * c->m, 0))) return rc;
     }
-    if (c->comm) {
-        // column-sharded ranks: every Ax_k is a sum over ranks
+    if (c->comm && !c->rows) {
+        // column-sharded ranks: every Ax_k is a sum over ranks (row shards: Ax rows are local)
         ncclResult_t nr = ncclAllReduce(p.Ax, p.Ax, (size_t)c->nblock * c->m, ncclFloat64, ncclSum, c->comm,
                                         c->stream);
         if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
@@ -777,9 +903,12 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
     {
         const char* why = c->onepass != 0 ? onepass_ineligible(c) : "disabled";
         if (c->onepass == 1 && why) return fail(BPGL_E_ARG, "onepass=1: %s", why);
+        if (c->rows && why) return fail(BPGL_E_ARG, "row shards run the one-pass iteration only: %s", why);
         c->op_on = c->onepass != 0 && !why;
         c->op_t = 0;
-        if (c->op_on && (rc = onepass_refresh(c))) return rc;
+        c->op_refresh_pending = false;
+        // external row shards: the caller runs the first exact gradient (phases 2 and 3)
+        if (c->op_on && !(c->rows && c->external) && (rc = onepass_refresh(c))) return rc;
     }
     drop_graphs(c);
     c->use_graph = use_graph != 0 && !c->external;

@@ -1,5 +1,5 @@
-// One-HBM-pass iteration (single feature block, single rank): A is streamed once per
-// iteration and yields both products the iteration needs.
+// One-HBM-pass iteration (single feature block; one rank, or row shards over ranks): A is
+// streamed once per iteration and yields both products the iteration needs.
 //
 // For one block the gradient obeys the recurrence
 //     g_{t+1} = A^T r_{t+1} = A^T (r_t + gamma_t s23_t) = g_t + gamma_t A^T (A D_t)
@@ -21,11 +21,18 @@
 //   * LAG rows later (the row is still in the register ring) every wave reads the SB
 //     granules of row t (lane = block; the load was issued PF rows earlier beside the row
 //     prefetch, so the in-order vmcnt queue is never drained), checks their tags and folds
-//     them in one fixed order -> s23[t], bit-identical in every block; U += row * s23[t];
+//     them in one fixed order -> s23[t], bit-identical in every block; U += row * s23[t]
+//     (SB <= 64: one granule per lane; SB <= 128: lanes l and l + 64, GPL = 2);
 //   * a late granule is re-polled (bounded; on exhaustion the state's op_fail word is set
 //     and the kernel still finishes -- bpgl_solver_status reports BPGL_E_EXCHANGE).
-// Outputs: s23 (by segment block 0) and one U partial row per row group; k_onepass_gupdate
-// folds the partials in a fixed order into g += gamma U after the line search.  Results are
+// Outputs: s23 (by segment block 0) and one U partial row per row group; k_onepass_tail
+// folds the partials in a fixed order into g += gamma U after the line search.
+//
+// Row shards (several ranks, bpgl_set_shard): rank q holds rows [m_q, m_{q+1}) of A and a
+// replicated copy of x, D, g (every column).  Then U = sum_q A_q^T (A_q D) and the line-search
+// dot products are sums over ranks: k_onepass_fold folds the row-group partials of this rank
+// into the exchange buffer [U (wp) | r.s23 | s23.s23], ONE all-reduce (SUM) of wp + 2 fp64
+// follows, and every rank computes the identical gamma, g, x and next D from it.  Results are
 // bitwise deterministic; the tag bit perturbs each s23 partial by <= 1 ulp (2^-52 relative).
 // Measured development steps: tools/onepass*_probe.hip, DESIGN.md section 6b.
 #pragma once
@@ -37,7 +44,7 @@ constexpr int kOpSlotsLog = 5;
 constexpr int kOpSlots = 1 << kOpSlotsLog;   // LDS partial slots (rows); > LAG + publication delay
 // an LDS slot's parity: row t and the slot's previous row t - kOpSlots differ in bit kOpSlotsLog
 constexpr int kOpDelta = 1;     // rows between a row's phase 1 and its publication
-constexpr int kOpMaxSB = 64;    // one granule per lane
+constexpr int kOpMaxSB = 128;   // at most two granules per lane (GPL)
 constexpr unsigned kOpPolls = 1u << 16;
 constexpr int kOpTailBlocks = 1024;   // k_onepass_tail grid cap (= its shrink partial count)
 
@@ -117,7 +124,7 @@ struct OnePassGeo {
     static constexpr int BC = kWaves * WC;   // columns per segment block
 };
 
-template <typename T, int NB, int PF, int LU>
+template <typename T, int NB, int PF, int LU, int GPL>
 __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o) {
     if (p.st->done) return;
     using G = OnePassGeo<LU, T>;
@@ -162,9 +169,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             u[k][e] = 0.0;
         }
     }
-    const int glane = lane < SB ? lane : 0;
+    static_assert(GPL == 1 || GPL == 2, "granules per lane");
+    int glane[GPL];   // granule k of this lane: segment block lane + 64 k
+#pragma unroll
+    for (int k = 0; k < GPL; ++k) glane[k] = lane + 64 * k < SB ? lane + 64 * k : 0;
     raw buf[NB][LU];
-    op_u64 gv[NB];
+    op_u64 gv[NB][GPL];
     unsigned polls = kOpPolls;
     bool failed = false;
 
@@ -177,7 +187,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     auto gload = [&](int t, int slot) {   // granules consumed at step t (phase 2 of row t - LAG)
         int t2 = t - LAG;
         t2 = t2 < 0 ? 0 : (t2 >= nrows ? nrows - 1 : t2);
-        gv[slot] = __hip_atomic_load(o.PG + (i0 + t2) * SB + glane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < GPL; ++k)
+            gv[slot][k] = __hip_atomic_load(o.PG + (i0 + t2) * SB + glane[k], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
     };
 
     // one row step: prefetch row t + PF (and the granules of its phase 2), phase 1 of row t,
@@ -222,21 +235,32 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         const int t2 = t - LAG;
         if (t2 >= 0 && t2 < nrows) {   // phase 2: U += row(t2) * s23[t2]
             const int qs = (q - LAG + NB) % NB;
-            op_u64 v = gv[q];
-            auto ready = [&](op_u64 g) { return lane >= SB || op_tag(g) == tag; };
-            if (!__all(ready(v))) {   // late: re-poll (drains this wave's queue; rare)
-                const op_u64* src = o.PG + (i0 + t2) * SB + glane;
+            op_u64 v[GPL];
+#pragma unroll
+            for (int k = 0; k < GPL; ++k) v[k] = gv[q][k];
+            auto ready = [&]() {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < GPL; ++k) ok = ok && (lane + 64 * k >= SB || op_tag(v[k]) == tag);
+                return ok;
+            };
+            if (!__all(ready())) {   // late: re-poll (drains this wave's queue; rare)
+                const op_u64* src = o.PG + (i0 + t2) * SB;
                 do {
                     if (polls == 0) { failed = true; break; }
                     --polls;
                     __builtin_amdgcn_s_sleep(2);
-                    v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } while (!__all(ready(v)));
+#pragma unroll
+                    for (int k = 0; k < GPL; ++k)
+                        v[k] = __hip_atomic_load(src + glane[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } while (!__all(ready()));
                 // settle here, so the merge with the fast path is not a pending load
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                asm volatile("" : "+v"(v));
+#pragma unroll
+                for (int k = 0; k < GPL; ++k) asm volatile("" : "+v"(v[k]));
             }
-            double x = lane < SB ? op_unstuff(v) : 0.0;
+            double x = lane < SB ? op_unstuff(v[0]) : 0.0;
+            if (GPL == 2) x += lane + 64 < SB ? op_unstuff(v[GPL - 1]) : 0.0;   // blocks l and l + 64, then the wave
             x = SB <= 16 ? op_lane(op_row_sum16(x), 0) : op_wave_sum(x);
             if (sb == 0 && wave == 0 && lane == 0) o.S[i0 + t2] = x;
 #pragma unroll
@@ -277,6 +301,31 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         if (colok[k])
 #pragma unroll
             for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
+}
+
+// Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23]
+// (fixed order over the row groups).  Runs whether or not the solver stopped: the all-reduce
+// after it runs in every iteration of a captured graph.
+__global__ __launch_bounds__(kThreads) void k_onepass_fold(Params p, OnePassArgs o, double* __restrict__ out) {
+    const long long stride = (long long)gridDim.x * kThreads;
+    for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < p.wp; j += stride) {
+        double acc = 0.0;
+        for (int q = 0; q < o.ngroups; ++q) acc += o.Us[(long long)q * p.wp + j];
+        out[j] = acc;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        double rs = 0.0, ss = 0.0;
+        for (int q = 0; q < o.ngroups; ++q) { rs += p.parts2[2ll * q]; ss += p.parts2[2ll * q + 1]; }
+        out[p.wp] = rs;
+        out[p.wp + 1] = ss;
+    }
+}
+
+// rec = 1 / diag after the column norms were summed over row shards (lasso.py:29-30)
+__global__ __launch_bounds__(kThreads) void k_recip(const double* __restrict__ d, double* __restrict__ rec,
+                                                    long long n) {
+    const long long j = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (j < n) rec[j] = 1.0 / d[j];
 }
 
 // Tail of a one-pass iteration, one kernel.  UPDATE: x += gamma D, Ax += gamma s23,

@@ -11,6 +11,17 @@ shrink is per column) and the partial s23 = A_g D_g; one RCCL all-reduce
 slots) then gives every rank the identical step size.  The all-reduce is
 issued by libbpgl on the solver stream (inside the captured graph).
 
+Row shards (``shard="rows"``, one feature block; no reference counterpart):
+rank g holds rows ``row_bounds(m, g, G)`` of A, its rows of b and of the
+residual, and a replicated x.  Every iteration streams the local A once
+(k_onepass: s23_g = A_g D and U_g = A_g^T s23_g together), and ONE all-reduce
+(SUM) of w_pad + 2 fp64 [U | r.s23 | s23.s23] gives every rank the identical
+gradient update g += gamma U and step size.  Column shards need A read twice
+per iteration (the exchange of s23 sits between the two products); row shards
+trade that second pass for a w-sized exchange, which is the better deal on
+xGMI whenever w * 8 B / (all-reduce bandwidth) < the pass time (configs[2]:
+4 MiB vs ~2 GiB of A per GPU).
+
 torch.distributed is only the side channel that carries the 128-byte RCCL
 unique id (gloo, CPU tensors); the data path never touches it.
 """
@@ -46,6 +57,28 @@ def shard_columns(A, Block, rank, nranks):
         return np.ascontiguousarray(np.concatenate(parts, axis=1))
     import torch
     return torch.cat(parts, dim=1).contiguous()
+
+
+def row_bounds(m, rank, nranks):
+    """Rows [start, stop) of rank `rank` (balanced; the first m % nranks ranks get one more)."""
+    if not 0 <= rank < nranks or m < nranks:
+        raise ValueError(f"cannot split {m} rows over {nranks} ranks")
+    q, r = divmod(m, nranks)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def shard_rows(A, rank, nranks):
+    """This rank's rows of A (numpy or torch; contiguous copy)."""
+    s, e = row_bounds(A.shape[0], rank, nranks)
+    if isinstance(A, np.ndarray):
+        return np.ascontiguousarray(A[s:e])
+    return A[s:e].contiguous()
+
+
+def row_exchange_layout(wp):
+    """Offsets in the row-shard all-reduce buffer (SUM over ranks)."""
+    return dict(u=(0, wp), rs=wp, ss=wp + 1, count=wp + 2)
 
 
 def assemble_x(x_shards, Block):

@@ -26,7 +26,11 @@ drivers never did (lasso.py:167-169, :609).
 
 Every compute call goes through libbpgl.so (``_native``); there is no
 alternative path.  Multi-GPU: pass ``comm=`` (see ``distributed.RankComm``);
-A is then this rank's column shard of every feature block.
+A is then this rank's column shard of every feature block (``shard="columns"``,
+the reference's P-way split), or, with ``shard="rows"`` and one feature block,
+this rank's rows of A (x replicated, one pass over A per iteration; see
+``distributed`` and include/bpgl.h ``bpgl_set_shard``).  In row mode the GEMV
+entry points return this rank's partial A_q^T r_q and its rows of A d.
 """
 import contextlib
 import ctypes
@@ -54,7 +58,10 @@ class GPU_Calculation:
     T_HEIGHT = 512
     TYPE = 'double'
 
-    def __init__(self, A, Block, device=None, comm=None):
+    def __init__(self, A, Block, device=None, comm=None, shard="columns"):
+        if shard not in ("columns", "rows"):
+            raise ValueError("shard must be 'columns' or 'rows'")
+        self.shard = shard
         self.Block = int(Block)
         self.MAT_WIDTH_ALL = int(A.shape[1])
         self.device = _resolve_device(A, device)
@@ -86,6 +93,8 @@ class GPU_Calculation:
                               ctypes.c_void_p(self.stream.cuda_stream)), "bpgl_create")
         self._ctx = ctx
         assert L.bpgl_block_width_padded(ctx) == Wp
+        if self.shard == "rows":
+            N.check(L.bpgl_set_shard(ctx, N.BPGL_SHARD_ROWS), "bpgl_set_shard")
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             At = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))
@@ -262,12 +271,20 @@ class GPU_Calculation:
     def set_ranks(self, rank, nranks):
         N.check(N.lib().bpgl_set_ranks(self._ctx, int(rank), int(nranks)), "bpgl_set_ranks")
 
+    def set_diag(self, diag):
+        """Install column norms computed elsewhere (external-exchange row shards: the sum of
+        every rank's own ``_diag``); also refreshes 1/diag."""
+        with self._on_stream():
+            self._diag.copy_(diag.reshape(self._diag.shape).to(self._diag))
+            N.check(N.lib().bpgl_set_diag(self._ctx, N.ptr(self._diag)), "bpgl_set_diag")
+
     def solver_phase(self, phase):
         with self._on_stream():
             N.check(N.lib().bpgl_solver_phase(self._ctx, int(phase)), "bpgl_solver_phase")
 
     def exchange_buffer(self):
-        """Device view of [s23 (m) | sum|Bx| | sum|x| | err slot per rank] (lives in the scratch)."""
+        """Device view of the per-iteration exchange (lives in the scratch): column shards
+        [s23 (m) | sum|Bx| | sum|x| | err slot per rank]; row shards [U (w_pad) | r.s23 | s23.s23]."""
         cnt = ctypes.c_int64()
         addr = N.lib().bpgl_solver_exchange_buffer(self._ctx, ctypes.byref(cnt))
         off = (addr - self._scratch.data_ptr()) // 8

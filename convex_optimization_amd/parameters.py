@@ -53,13 +53,14 @@ def parameters(N, K, den, SAVE_FLAG=False, READ_FLAG=False, SILENCE=False, seed=
 
 
 def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal_cls=None, comm=None,
-                    col_range=None):
+                    col_range=None, row_range=None):
     """Build (gpu_cal, b, mu, x_true) with A generated in HBM.
 
     A is drawn with torch's CUDA generator in fp32, its rows scaled to unit
     norm, and stored as ``TYPE``.  b = A x_true + 0.01 e is formed with the
     package's own A.d kernel (fp64), mu = 0.1 ||A^T b||_inf with its A^T r
-    kernel.  ``col_range``/``comm``: build only this rank's column shard (the
+    kernel.  ``row_range=(start, stop)``: this rank's rows only (row shards, one
+    block; b is local, A^T b summed over ranks).  ``col_range``/``comm``: build only this rank's column shard (the
     full row normalisation is computed from row sums all ranks agree on).
     """
     import torch
@@ -76,6 +77,12 @@ def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal
     x_true = torch.where(mask, torch.randn(K, generator=xg, device=dev, dtype=torch.float64),
                          torch.zeros((), dtype=torch.float64, device=dev))
     e = 0.01 * torch.randn(N, generator=xg, device=dev, dtype=torch.float64)
+    if row_range is not None:
+        if col_range is not None or Block != 1:
+            raise ValueError("row shards take one feature block and no column range")
+        r0, r1 = int(row_range[0]), int(row_range[1])
+        A = A[r0:r1].clone()
+        e = e[r0:r1]
     if col_range is not None:
         A = A[:, col_range].contiguous()
         x_loc = x_true[col_range]
@@ -87,7 +94,7 @@ def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal
     old = cls.TYPE
     cls.TYPE = TYPE
     try:
-        gc = cls(A, Block, device=dev, comm=comm)
+        gc = cls(A, Block, device=dev, comm=comm, shard="rows" if row_range is not None else "columns")
     finally:
         cls.TYPE = old
     del A
@@ -97,7 +104,7 @@ def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal
     for k in range(Block):
         gc.matMulVec_DiffSize(tmp, k, x_loc[k * W:(k + 1) * W])
         b += tmp
-    if comm is not None and comm.world > 1:
+    if comm is not None and comm.world > 1 and row_range is None:
         import torch.distributed as dist
         bc = b.cpu()
         dist.all_reduce(bc, group=comm.group)
@@ -107,6 +114,11 @@ def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal
     gt = torch.empty(W, dtype=torch.float64, device=dev)
     for k in range(Block):
         gc.mat_tMulVec_DiffSize(gt, k, b)
+        if row_range is not None and comm is not None and comm.world > 1:
+            import torch.distributed as dist
+            gp = gt.cpu()                      # this rank's rows' share of A^T b
+            dist.all_reduce(gp, group=comm.group)
+            gt = gp.to(dev)
         gmax = torch.maximum(gmax, gt.abs().max())
     if comm is not None and comm.world > 1:
         import torch.distributed as dist

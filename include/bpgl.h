@@ -88,6 +88,13 @@ int bpgl_bind(bpgl_ctx* ctx, const void* A, int64_t lda, int64_t block_stride,
 int bpgl_diag_ata(bpgl_ctx* ctx, double* out);
 
 /*
+ * Install diag(A_b^T A_b) (device, nblock * w_pad fp64) computed elsewhere, and
+ * 1/diag.  Used by external-exchange row shards, whose column norms are sums of
+ * every rank's bpgl_diag_ata output (the RCCL path does that sum itself).
+ */
+int bpgl_set_diag(bpgl_ctx* ctx, const double* diag);
+
+/*
  * g = A_b^T r  (device: r has m fp64 values, g receives w_pad fp64 values).
  * Replaces GPU_Calculation.mat_tMulVec_DiffSize + kernel mul_mat_t_vec_diffsize
  * (gpu_calculation.py:264-277, :20-55); the split-K reduction happens on the
@@ -114,6 +121,19 @@ int bpgl_comm_unique_id(void* out128);
 int bpgl_comm_init(bpgl_ctx* ctx, const void* unique_id128, int rank, int nranks);
 
 /*
+ * Shard layout across ranks (call between bpgl_create and bpgl_bind):
+ * BPGL_SHARD_COLUMNS (default) as above; BPGL_SHARD_ROWS: one feature block, rank
+ * q holds rows [m_q, m_{q+1}) of A (the context's m is its row count, n_local the
+ * full width), b and the residual are local, x is replicated.  Row shards run the
+ * one-pass iteration (A read once per iteration): per iteration one all-reduce
+ * (SUM) of w_pad + 2 fp64 [A^T A D | r.s23 | s23.s23]; bpgl_diag_ata and every
+ * exact gradient refresh all-reduce w_pad values.  There is no reference
+ * counterpart: the reference shards columns only (cpu_calculation.py:23-27).
+ */
+enum { BPGL_SHARD_COLUMNS = 0, BPGL_SHARD_ROWS = 1 };
+int bpgl_set_shard(bpgl_ctx* ctx, int mode);
+
+/*
  * Caller-performed exchange (validation of the sharded kernels where RCCL
  * cannot run, e.g. several ranks on one GPU): bpgl_set_ranks declares this
  * context rank `rank` of `nranks` without a communicator.  Each iteration is
@@ -122,6 +142,10 @@ int bpgl_comm_init(bpgl_ctx* ctx, const void* unique_id128, int rank, int nranks
  * writes the sum back on every rank; bpgl_solver_phase(ctx, 1).  Requires the
  * initial point x = 0.
  */
+/* Row shards (count = w_pad + 2): the same two phases per iteration; in
+ * addition the exact gradient g = A^T r is exchanged by phase 2 (this rank's
+ * A_q^T r_q into the exchange buffer), the caller's sum, and phase 3 -- after
+ * bpgl_solver_reset and again every "onepass_refresh" iterations. */
 int bpgl_set_ranks(bpgl_ctx* ctx, int rank, int nranks);
 int bpgl_solver_phase(bpgl_ctx* ctx, int phase);
 double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
@@ -165,7 +189,8 @@ int bpgl_iterate(bpgl_ctx* ctx, int64_t n_iter, const int32_t* order, double mu,
  * kinds: 0 colpass (A^T r), 1 shrink, 2 rowpass (A D), 3 rowreduce (+ line
  * search on one rank), 4 allreduce, 5 step (multi-rank line search), 6 update
  * (+ gradient update in one-pass mode), 7 onepass (A D and A^T (A D) in one
- * pass over A). */
+ * pass over A).  Row shards: 3 = fold of the exchange contribution, 5 = line
+ * search. */
 int bpgl_set_kernel_timing(bpgl_ctx* ctx, int enable);
 int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
 
@@ -180,9 +205,9 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
  * each path is bitwise deterministic):
  *   "onepass" (default -1 = when eligible, 0 = off, 1 = required): one pass
  *   over A per iteration, the gradient carried as g += gamma A^T (A D); needs
- *   one feature block, one rank, no fused mode, at most 64 x 4096 columns
- *   (fp32/bf16; 64 x 2048 for fp64) and all of its blocks resident at once
- *   (nothing else running on the device).
+ *   one feature block, one rank (or row shards), no fused mode, at most
+ *   128 x 4096 columns (fp32/bf16; 128 x 2048 for fp64) and all of its blocks
+ *   resident at once (nothing else running on the device).
  *   "onepass_refresh" (default 64; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "fused" (default 0): the two-launch fused iteration.

@@ -119,3 +119,81 @@ def test_sharded_exchange_protocol_matches_single_rank():
     ref = oracle.run(A, fx["b"], float(fx["mu"]), int(fx["BLOCK"]), 60)["x"]
     x = D.assemble_x([np.array(out[0]), np.array(out[1])], int(fx["BLOCK"]))
     assert np.linalg.norm(x - ref) <= 1e-10 * np.linalg.norm(ref)
+
+
+def test_row_bounds_cover_and_balance():
+    for m, G in [(10, 3), (8192, 8), (7, 7), (1001, 4)]:
+        b = [D.row_bounds(m, g, G) for g in range(G)]
+        assert b[0][0] == 0 and b[-1][1] == m
+        assert all(b[g][1] == b[g + 1][0] for g in range(G - 1))
+        sizes = [e - s for s, e in b]
+        assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        D.row_bounds(3, 0, 4)
+    A = np.arange(20.0).reshape(5, 4)
+    np.testing.assert_array_equal(np.concatenate([D.shard_rows(A, g, 2) for g in range(2)]), A)
+    assert D.row_exchange_layout(16) == dict(u=(0, 16), rs=16, ss=17, count=18)
+
+
+def _row_rank_iterations(A_loc, b_loc, mu, iters, refresh):
+    """One rank of the row-sharded one-pass solver, restating the device kernels' per-rank
+    work (k_onepass, k_onepass_fold, k_linesearch, k_onepass_tail; colpass + all-reduce for the
+    exact gradient) with the gloo all-reduce standing in for RCCL."""
+    def allreduce(v):
+        t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64))
+        dist.all_reduce(t)
+        return t.numpy()
+
+    w = A_loc.shape[1]
+    dg = allreduce(np.square(A_loc).sum(axis=0))
+    x = np.zeros(w)
+    Ax = np.zeros(A_loc.shape[0])
+    r = Ax - b_loc
+    g = allreduce(A_loc.T @ r)
+
+    def shrink(g, x):
+        rx = dg * x - g
+        bx = np.sign(rx) * np.maximum(np.abs(rx) - mu, 0) / dg
+        return bx, bx - x
+    bx, Dv = shrink(g, x)
+    lay = D.row_exchange_layout(w)
+    for t in range(iters):
+        if refresh and t and t % refresh == 0:
+            g = allreduce(A_loc.T @ r)
+            bx, Dv = shrink(g, x)
+        s23 = A_loc @ Dv
+        buf = np.zeros(lay["count"])
+        buf[:w] = A_loc.T @ s23
+        buf[lay["rs"]] = r @ s23
+        buf[lay["ss"]] = s23 @ s23
+        buf = allreduce(buf)
+        r1 = buf[lay["rs"]] + mu * (np.abs(bx).sum() - np.abs(x).sum())
+        r2 = buf[lay["ss"]]
+        gamma = 0.0 if r2 == 0 else min(max(-r1 / r2, 0.0), 1.0)
+        x = x + gamma * Dv
+        Ax = Ax + gamma * s23
+        r = Ax - b_loc
+        g = g + gamma * buf[:w]
+        bx, Dv = shrink(g, x)
+    return x
+
+
+def _row_solver_worker(rank, world, port, out):
+    _init(rank, world, port)
+    fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "c1_b1_p1_f32in.npz")))
+    A = oracle.fixture_A(fx)
+    s, e = D.row_bounds(A.shape[0], rank, world)
+    out[rank] = _row_rank_iterations(D.shard_rows(A, rank, world), fx["b"].reshape(-1)[s:e],
+                                     float(fx["mu"]), 120, refresh=50).tolist()
+    dist.destroy_process_group()
+
+
+def test_row_sharded_exchange_protocol_matches_reference():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    _spawn(_row_solver_worker, 2, out)
+    fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "c1_b1_p1_f32in.npz")))
+    A = oracle.fixture_A(fx)
+    ref = oracle.run(A, fx["b"], float(fx["mu"]), 1, 120)["x"]
+    np.testing.assert_array_equal(np.array(out[0]), np.array(out[1]))   # x replicated bit for bit
+    assert np.linalg.norm(np.array(out[0]) - ref) <= 1e-9 * np.linalg.norm(ref)

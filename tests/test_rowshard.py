@@ -1,0 +1,161 @@
+"""Row shards (include/bpgl.h bpgl_set_shard, bpgl_onepass.h k_onepass_fold): rank q holds
+rows [m_q, m_{q+1}) of the single feature block, x is replicated, each iteration streams the
+local A once and all-reduces [U | r.s23 | s23.s23] (w_pad + 2 fp64).
+
+The reference has no row split (it shards columns, cpu_calculation.py:23-27); the iteration
+it computes is the same (lasso.py:102-157), so parity is against the reference's fixtures and
+the single-rank solver.  Several ranks cannot share one GPU under RCCL, so the multi-rank
+cases here run the ranks' kernels on one GPU with the exchange done by the test (phases 0/1
+per iteration, 2/3 for the exact-gradient refresh); the RCCL leg runs with one rank.
+Tolerances (relative l2 on x): reference fixtures <= 1e-9 (as every solver test); rank
+counts against each other and against the single-rank one-pass path <= 1e-10 (the sums over
+ranks change the fp64 summation order only)."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from convex_optimization_amd import _native as N  # noqa: E402
+from convex_optimization_amd import distributed as D  # noqa: E402
+from convex_optimization_amd.gpu_calculation import GPU_Calculation  # noqa: E402
+
+
+def make_cls(type_name):
+    return type("GC_" + type_name, (GPU_Calculation,), {"TYPE": type_name})
+
+
+def rel(a, b):
+    a, b = np.asarray(a).reshape(-1), np.asarray(b).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def _exchange(ranks):
+    torch.cuda.synchronize()
+    total = sum(gc.exchange_buffer().clone() for gc in ranks)
+    for gc in ranks:
+        gc.exchange_buffer().copy_(total)
+    torch.cuda.synchronize()
+
+
+def run_external(A, b, mu, world, iters, type_name="float", err_bound=None, refresh=64):
+    """`world` row-shard ranks on one GPU, the all-reduce done here."""
+    ranks = []
+    for g in range(world):
+        gc = make_cls(type_name)(D.shard_rows(A, g, world), 1, device=0, shard="rows")
+        gc.set_ranks(g, world)
+        gc.set_tuning("onepass_refresh", refresh)
+        ranks.append(gc)
+    diag = sum(gc._diag.clone() for gc in ranks)   # column norms: sums over ranks
+    for g, gc in enumerate(ranks):
+        gc.set_diag(diag)
+        s, e = D.row_bounds(A.shape[0], g, world)
+        gc.solver_reset(np.asarray(b).reshape(-1)[s:e], mu, err_bound=err_bound, record_len=iters,
+                        use_graph=False)
+
+    def refresh_g():
+        for gc in ranks:
+            gc.solver_phase(2)
+        _exchange(ranks)
+        for gc in ranks:
+            gc.solver_phase(3)
+
+    refresh_g()
+    for t in range(iters):
+        if refresh and t and t % refresh == 0:
+            refresh_g()
+        for gc in ranks:
+            gc.solver_phase(0)
+        _exchange(ranks)
+        for gc in ranks:
+            gc.solver_phase(1)
+    return ranks
+
+
+@pytest.mark.parametrize("case,world,type_name", [("c1_b1_p1_f32in", 2, "float"), ("c1_b1_p1_f32in", 4, "float"),
+                                                  ("c1_b1_p1_f64", 3, "double")])
+def test_external_row_ranks_match_reference(golden, case, world, type_name):
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    IT = int(fx["ITER_MAX"])
+    ranks = run_external(A, fx["b"], float(fx["mu"]), world, IT, type_name=type_name)
+    xs = [gc.solver_x() for gc in ranks]
+    for x in xs[1:]:
+        np.testing.assert_array_equal(x, xs[0])          # x is replicated bit for bit
+    assert rel(xs[0], fx["x"]) <= 1e-9, rel(xs[0], fx["x"])
+    errs = [gc.solver_records()[0] for gc in ranks]
+    np.testing.assert_array_equal(errs[0], errs[-1])
+    np.testing.assert_allclose(errs[0][:IT], fx["err_iter"][:IT], rtol=1e-6, atol=1e-9)
+
+
+def test_external_row_ranks_ragged_and_stop():
+    """rows not divisible by the rank count; the err_bound stop fires on every rank at the same t"""
+    rs = np.random.RandomState(21)
+    m, n = 1001, 5000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.1, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    single = make_cls("float")(A, 1, device=0)
+    ref = single.run(b, mu, 300, err_bound=1e-4)
+    ranks = run_external(A, b, mu, 3, 300, err_bound=1e-4)
+    st = [gc.solver_status() for gc in ranks]
+    assert ref["stopped"] and all(s["stopped"] for s in st)
+    assert all(s["t_last"] == ref["t_last"] for s in st), (ref["t_last"], [s["t_last"] for s in st])
+    assert rel(ranks[0].solver_x(), ref["x"]) <= 1e-10, rel(ranks[0].solver_x(), ref["x"])
+
+
+def test_single_rank_rccl_rows_matches_onepass():
+    """the RCCL leg (comm init, all-reduce of [U | r.s23 | s23.s23] inside the graph, the
+    w-sized diag and gradient all-reduces) with one rank: same iterates as the plain solver"""
+    rs = np.random.RandomState(8)
+    m, n = 1500, 12000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    plain = make_cls("float")(A, 1, device=0).run(b, mu, 150)
+    rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    np.testing.assert_allclose(rows.diag_ATA, make_cls("float")(A, 1, device=0).diag_ATA, rtol=1e-15)
+    g1 = rows.run(b, mu, 150, use_graph=True)
+    g0 = rows.run(b, mu, 150, use_graph=False)
+    np.testing.assert_array_equal(g1["x"], g0["x"])
+    assert g1["iters"] == 150
+    assert rel(g1["x"], plain["x"]) <= 1e-10, rel(g1["x"], plain["x"])
+
+
+def test_two_granules_per_lane_width():
+    """SB > 64 segment blocks per row (two hand-off granules per lane), the per-GPU shape of
+    configs[2] under row shards at 8 GPUs (1024 x 524288 fp32), one rank"""
+    from convex_optimization_amd.parameters import device_instance
+    gc, b, mu, _ = device_instance(1024, 524288, 0.4, 1, TYPE="float", seed=3, device=0)
+    gc.set_tuning("onepass", 1)
+    one = gc.run(b, mu, 10)
+    gc.set_tuning("onepass", 0)
+    two = gc.run(b, mu, 10)
+    assert rel(one["x"], two["x"]) <= 1e-10, rel(one["x"], two["x"])
+    rows = make_cls("float")(gc._A_dev, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    r = rows.run(b, mu, 10)
+    assert rel(r["x"], one["x"]) <= 1e-12, rel(r["x"], one["x"])
+
+
+def test_row_shard_argument_errors():
+    A = np.random.RandomState(0).randn(64, 256)
+    with pytest.raises(N.BpglError, match="one feature block"):
+        make_cls("float")(A, 2, device=0, shard="rows")
+    with pytest.raises(ValueError):
+        make_cls("float")(A, 1, device=0, shard="diagonal")
+    gc = make_cls("float")(A, 1, device=0, shard="rows")
+    gc.set_tuning("onepass", 0)
+    with pytest.raises(N.BpglError, match="row shards run the one-pass iteration only"):
+        gc.run(np.ones(64), 0.1, 3)
+    gc.set_tuning("onepass", -1)
+    gc.solver_reset(np.ones(64), 0.1)
+    with pytest.raises(N.BpglError, match="external row shards"):
+        gc.solver_phase(2)
+    # bind already happened: the layout is fixed
+    with pytest.raises(N.BpglError, match="precede"):
+        N.check(N.lib().bpgl_set_shard(gc._ctx, N.BPGL_SHARD_COLUMNS), "bpgl_set_shard")
