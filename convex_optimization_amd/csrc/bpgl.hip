@@ -132,7 +132,8 @@ void geometry(bpgl_ctx* c) {
         c->op_ngroups = (int)ng;
         c->op_R = (int)R;
         c->op_xl = (ng % 8 == 0) ? 1 : 0;   // each row group's blocks on one XCD (blockIdx % 8)
-        c->op_tail_grid = (int)std::min<int64_t>(cdiv(std::max<int64_t>(c->m, c->wp), kThreads), kOpTailBlocks);
+        // k_onepass_tail: 64-column tiles and 256-row strides
+        c->op_tail_grid = (int)std::min<int64_t>(std::max(cdiv(c->m, kThreads), cdiv(c->wp, 64)), kOpTailBlocks);
     } else {
         c->op_SB = c->op_ngroups = c->op_R = c->op_xl = c->op_tail_grid = 0;
     }
@@ -277,6 +278,15 @@ template <> struct OpVar<bf16_t, 2> { static constexpr int NB = 22, PF = 6; };
 template <> struct OpVar<bf16_t, 3> { static constexpr int NB = 18, PF = 6; };
 constexpr int kOpVariants = 4;
 
+// the two-pass kernels' view of one-pass state: g is read from G (one slab row), s23 from S
+Params op_params(const bpgl_ctx* c) {
+    Params q = c->p;
+    q.slab_g = c->op.G;
+    q.nchunk = 1;
+    q.nseg = 1;
+    q.nparts = c->op_tail_grid;   // shrink partials come from k_onepass_tail
+    return q;
+}
 // GPL: granules per lane of the row hand-off (SB <= 64: 1, SB <= 128: 2)
 template <typename T, int V, int GPL>
 const void* onepass_fn_v() { return (const void*)k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU, GPL>; }
@@ -298,7 +308,7 @@ const void* onepass_fn(int dtype, int v, int gpl) {
 template <typename T, int V, int GPL>
 void onepass_launch_v(bpgl_ctx* c) {
     hipLaunchKernelGGL((k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU, GPL>),
-                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, c->p, c->op);
+                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, op_params(c), c->op);
 }
 template <typename T, int GPL>
 void onepass_launch_g(bpgl_ctx* c) {
@@ -322,15 +332,6 @@ int onepass_launch(bpgl_ctx* c) {
     }
     LAUNCH_CHECK("k_onepass");
     return 0;
-}
-// the two-pass kernels' view of one-pass state: g is read from G (one slab row), s23 from S
-Params op_params(const bpgl_ctx* c) {
-    Params q = c->p;
-    q.slab_g = c->op.G;
-    q.nchunk = 1;
-    q.nseg = 1;
-    q.nparts = c->op_tail_grid;   // shrink partials come from k_onepass_tail
-    return q;
 }
 // the one-pass tail's view of U: the row-group partials (one rank), or the all-reduced sum
 // in the exchange buffer (row shards)
@@ -448,9 +449,9 @@ int finalize_fused(bpgl_ctx* c) {
 // phase 0: colpass, shrink, rowpass, rowreduce [, allreduce, step]; phase 1: update.
 // With the caller doing the exchange (external ranks) phase 0 stops after
 // rowreduce and phase 1 starts with the step.
-// one-pass iteration, three kernels: k_onepass (s23 and the U partials; its row groups also
-// fold r.s23 and s23.s23), k_linesearch; phase 1: k_onepass_tail (x, Ax, r, g += gamma U and
-// the next iteration's shrink)
+// one-pass iteration, two kernels: k_onepass (s23 and the U partials; its row groups also
+// fold r.s23 and s23.s23, and the last group to finish runs the line search); phase 1:
+// k_onepass_tail (x, Ax, r, g += gamma U and the next iteration's shrink)
 //
 // Row shards: k_onepass, k_onepass_fold -> exchange buffer, all-reduce (RCCL), k_linesearch on
 // the summed scalars; phase 1: k_onepass_tail with the summed U.  With the exchange done by the
@@ -491,14 +492,10 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
 int enqueue_phase_onepass(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
     if (c->rows) return enqueue_phase_onepass_rows(c, it, phase);
-    if (phase == 0) {
+    if (phase == 0) {   // k_onepass ends with the line search (its last row group)
         ev_record(c, it, 7, 0);
         if ((rc = onepass_launch(c))) return rc;
         ev_record(c, it, 7, 1);
-        ev_record(c, it, 3, 0);
-        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, op_params(c), c->op_ngroups);
-        LAUNCH_CHECK("k_linesearch");
-        ev_record(c, it, 3, 1);
     } else {
         ev_record(c, it, 6, 0);
         if ((rc = onepass_tail<true>(c))) return rc;
@@ -697,6 +694,7 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
         c->op.ngroups = c->op_ngroups;
         c->op.R = c->op_R;
         c->op.xl = c->op_xl;
+        c->op.ls = c->rows ? 0 : 1;   // row shards: the line search follows the all-reduce
     }
     HIP_TRY(hipSetDevice(c->device));
     if (c->op_shape) HIP_TRY(hipMemsetAsync(s + L.opPG, 0, 8 * c->m * c->op_SB, c->stream));   // tag 0: never written

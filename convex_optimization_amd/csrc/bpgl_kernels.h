@@ -43,6 +43,7 @@ struct DevState {
     unsigned long long cnt_all;         // fused mode: arrivals of row-chunk finishers in k_iter_b
     long long op_epoch;   // one-pass mode: launches so far (tag of the row-partial hand-off)
     long long op_fail;    // one-pass mode: a hand-off poll ran out (blocks not co-resident)
+    unsigned long long op_cnt;   // one-pass mode: row-group arrivals (k_onepass line search)
 };
 
 struct Params {
@@ -736,6 +737,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(Params p) {
         DevState* st = p.st;
         st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0; st->pending = 0;
         st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0; st->op_fail = 0;
+        st->op_cnt = 0;
         st->t_base = (long long)wall_clock64();
         if (p.time_iter) p.time_iter[0] = 0.0;
     }

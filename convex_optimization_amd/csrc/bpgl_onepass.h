@@ -54,6 +54,7 @@ struct OnePassArgs {
     double* Us;                  // [ngroups][wp] U partial of each row group
     unsigned long long* PG;      // [m][SB] tagged row partials
     int SB, ngroups, R, xl;      // segment blocks per row, row groups, rows per group, XCD-local map
+    int ls;                      // 1: the last row group to finish runs the line search (one rank)
 };
 
 typedef unsigned long long op_u64;
@@ -116,6 +117,40 @@ __device__ __forceinline__ double op_quad_sum(double x) {
     return x;
 }
 
+// The line search of a one-rank one-pass iteration (lasso.py:129-150), run by the last row
+// group of k_onepass to finish: its r.s23 / s23.s23 partials (parts2, written through to
+// memory by every group) and the shrink partials of the previous k_onepass_tail, folded in
+// a fixed order.  The arrival counter only grows: launch k ends at count k * ngroups.
+__device__ __forceinline__ bool op_arrive_last(unsigned long long* cnt, unsigned long long expected) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = ((old + 1) % expected) == 0;
+    }
+    __syncthreads();
+    return last != 0;
+}
+__device__ void op_linesearch(const Params& p, int ngroups) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double rs = 0.0, ss = 0.0;
+    for (int k = threadIdx.x; k < ngroups; k += kThreads) {
+        rs += ld_sc1(p.parts2 + 2ll * k);
+        ss += ld_sc1(p.parts2 + 2ll * k + 1);
+    }
+    __shared__ double sr[kWaves], sq[kWaves];
+    rs = wave_sum(rs);
+    ss = wave_sum(ss);
+    if (lane == 0) { sr[wave] = rs; sq[wave] = ss; }
+    __syncthreads();
+    rs = ((sr[0] + sr[1]) + sr[2]) + sr[3];
+    ss = ((sq[0] + sq[1]) + sq[2]) + sq[3];
+    double a, b, e;
+    fold_parts(p, p.nparts, a, b, e);
+    if (threadIdx.x == 0) finish_step(p, rs, ss, a, b, e);
+}
+
 template <int LU, typename T>
 struct OnePassGeo {
     static constexpr int N = VecT<T>::N;
@@ -144,7 +179,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     const long long i1 = i0 + o.R < p.m ? i0 + o.R : p.m;
     const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
     if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
-        if (sb == 0 && threadIdx.x == 0) { p.parts2[2ll * grp] = 0.0; p.parts2[2ll * grp + 1] = 0.0; }
+        if (sb == 0 && threadIdx.x == 0) { st_sc1(p.parts2 + 2ll * grp, 0.0); st_sc1(p.parts2 + 2ll * grp + 1, 0.0); }
+        if (o.ls && sb == 0 && op_arrive_last(&p.st->op_cnt, (unsigned long long)o.ngroups))
+            op_linesearch(p, o.ngroups);
         return;
     }
     const unsigned tag = (unsigned)((p.st->op_epoch + 1) & 1);   // bound scratch is zero: parity 0 = unwritten
@@ -293,7 +330,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         }
         rs = op_wave_sum(rs);
         ss = op_wave_sum(ss);
-        if (lane == 0) { p.parts2[2ll * grp] = rs; p.parts2[2ll * grp + 1] = ss; }
+        if (lane == 0) { st_sc1(p.parts2 + 2ll * grp, rs); st_sc1(p.parts2 + 2ll * grp + 1, ss); }
     }
     double* dst = o.Us + (long long)grp * p.wp;
 #pragma unroll
@@ -301,6 +338,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         if (colok[k])
 #pragma unroll
             for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
+    if (o.ls && sb == 0 && op_arrive_last(&p.st->op_cnt, (unsigned long long)o.ngroups))   // block-uniform
+        op_linesearch(p, o.ngroups);
 }
 
 // Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23]
@@ -332,7 +371,7 @@ __global__ __launch_bounds__(kThreads) void k_recip(const double* __restrict__ d
 // r = Ax - b (lasso.py:153-155, :105), g += gamma sum_groups U (fixed order); then, for every
 // mode, the shrink of the next iteration from (g, x) (lasso.py:114-119, cpu_calculation.py:
 // 15-20): D, g mirrored to p.g, and per-block [sum|Bx|, sum|x|, max err] partials that
-// k_linesearch folds (p.nparts = gridDim.x).  UPDATE = false runs the shrink alone (after a
+// the next line search folds (p.nparts = gridDim.x).  UPDATE = false runs the shrink alone (after a
 // reset or an exact refresh of g).  UPDATE also advances the launch parity iff k_onepass ran
 // (it runs in the iteration whose line search stops, too).
 template <bool UPDATE>
@@ -352,53 +391,66 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
             p.r[k] = ax - p.b[k];
         }
     }
+    // columns: tiles of 64 (lane = column); the 4 waves split the row-group partials of U
+    // (q = wave, wave + 4, ...), wave 0 adds the 4 sums in a fixed order and runs the shrink
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ double ured[kWaves][64];
     double abx = 0.0, ax1 = 0.0, err = 0.0;
-    for (long long j = k0; j < p.wp; j += stride) {
-        double g = o.G[j];
+    const long long ntile = (p.wp + 63) / 64;
+    for (long long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {   // block-uniform
+        const long long j = tile * 64 + lane;
+        const bool ok = j < p.wp;
         if (UPDATE) {
             double acc = 0.0;
-            for (int q = 0; q < o.ngroups; ++q) acc += o.Us[(long long)q * p.wp + j];
-            g += gamma * acc;
-            o.G[j] = g;
-        }
-        p.g[j] = g;
-        double Dj = 0.0;
-        if (j < p.w) {
-            double xj = p.x[j];
-            if (UPDATE) {
-                xj += gamma * p.D[j];
-                p.x[j] = xj;
+            if (ok) {
+#pragma unroll 4
+                for (int q = wave; q < o.ngroups; q += kWaves) acc += o.Us[(long long)q * p.wp + j];
             }
-            const double rx = p.diag[j] * xj - g;                 // lasso.py:114
-            const double bx = p.rec[j] * soft_thr(rx, p.mu);      // lasso.py:115-117
-            Dj = bx - xj;                                         // lasso.py:119
-            abx += fabs(bx);
-            ax1 += fabs(xj);
-            const double e = fabs(g - proj(g - xj, -p.mu, p.mu)); // cpu_calculation.py:15-20
-            err = (e > err || e != e) ? e : err;
+            ured[wave][lane] = acc;
+            __syncthreads();
         }
-        p.D[j] = Dj;
+        if (wave == 0 && ok) {
+            double g = o.G[j];
+            if (UPDATE) {
+                g += gamma * (((ured[0][lane] + ured[1][lane]) + ured[2][lane]) + ured[3][lane]);
+                o.G[j] = g;
+            }
+            p.g[j] = g;
+            double Dj = 0.0;
+            if (j < p.w) {
+                double xj = p.x[j];
+                if (UPDATE) {
+                    xj += gamma * p.D[j];
+                    p.x[j] = xj;
+                }
+                const double rx = p.diag[j] * xj - g;                 // lasso.py:114
+                const double bx = p.rec[j] * soft_thr(rx, p.mu);      // lasso.py:115-117
+                Dj = bx - xj;                                         // lasso.py:119
+                abx += fabs(bx);
+                ax1 += fabs(xj);
+                const double e = fabs(g - proj(g - xj, -p.mu, p.mu)); // cpu_calculation.py:15-20
+                err = (e > err || e != e) ? e : err;
+            }
+            p.D[j] = Dj;
+        }
+        if (UPDATE) __syncthreads();   // ured is rewritten by the next tile
     }
-    abx = wave_sum(abx);
-    ax1 = wave_sum(ax1);
-    err = wave_max(err);
-    __shared__ double red[3][kWaves];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) { red[0][wave] = abx; red[1][wave] = ax1; red[2][wave] = err; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double e = red[2][0];
-        for (int q = 1; q < kWaves; ++q) e = (red[2][q] > e || red[2][q] != red[2][q]) ? red[2][q] : e;
-        double* dst = p.parts + 4ll * blockIdx.x;
-        dst[0] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-        dst[1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-        dst[2] = e;
-        dst[3] = 0.0;
-        if (UPDATE && blockIdx.x == 0) {
-            const long long t = p.st->t - 1;
-            p.st->iters = t + 1;
-            if (p.time_iter && t < p.rec_len)
-                p.time_iter[t + 1] = (double)(wall_clock64() - p.st->t_base) * p.wall_tick_s;
+    if (wave == 0) {
+        abx = wave_sum(abx);
+        ax1 = wave_sum(ax1);
+        err = wave_max(err);
+        if (lane == 0) {
+            double* dst = p.parts + 4ll * blockIdx.x;
+            dst[0] = abx;
+            dst[1] = ax1;
+            dst[2] = err;
+            dst[3] = 0.0;
+            if (UPDATE && blockIdx.x == 0) {
+                const long long t = p.st->t - 1;
+                p.st->iters = t + 1;
+                if (p.time_iter && t < p.rec_len)
+                    p.time_iter[t + 1] = (double)(wall_clock64() - p.st->t_base) * p.wall_tick_s;
+            }
         }
     }
 }
