@@ -454,6 +454,9 @@ def main():
             "iter_roofline_frac": iters_s_graph * it_bytes / (HBM_PEAK_GBS * 1e9),
             "two_pass_alg_bytes_per_iter_per_gpu": alg_bytes_iter(ml, w, sa),
             "two_pass_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(ml, w, sa),
+            # SURVEY 8d's iteration roofline (two passes over A): > 1 means the one-pass iteration
+            # beats what any two-pass implementation could reach at 8 TB/s
+            "two_pass_iter_roofline_frac": iters_s_graph * alg_bytes_iter(ml, w, sa) / (HBM_PEAK_GBS * 1e9),
             "launch_mode": "hipGraph replay of one iteration (value); eager + HIP events (kernel times)", "fused": args.fused,
             "iters_per_s_eager_with_events": iters_s_ev,
             "kernel_avg_ms": kms,

@@ -38,9 +38,7 @@ def per_launch(dirname, counter):
                     key = "k_colpass"
                 elif "k_rowpass" in name:
                     key = "k_rowpass"
-                elif "k_onepass_gupdate" in name:
-                    continue
-                elif "k_onepass" in name:
+                elif "k_onepass<" in name:      # not k_onepass_tail / k_onepass_fold
                     key = "k_onepass"
                 elif "k_panel_pass1" in name:
                     key = "k_panel_pass1"
@@ -66,7 +64,7 @@ def main():
         if alg:
             out[k]["alg_bytes"] = alg
             out[k]["traffic_over_alg"] = (fb + wb) / alg
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = os.environ.get("PMC_OUT") or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = {}
     if os.path.exists(path):
         data = json.load(open(path))
