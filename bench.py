@@ -87,6 +87,8 @@ def parse():
     ap.add_argument("--onepass", type=int, default=-1, choices=[-1, 0, 1],
                     help="one pass over A per iteration: -1 (default) when eligible (1 block, 1 rank), 0 off, 1 required")
     ap.add_argument("--onepass-variant", type=int, default=0, help="one-pass ring depth / prefetch variant (0-3)")
+    ap.add_argument("--onepass-cache", type=int, default=-1,
+                    help="permille of each one-pass row group read with cache-allocating loads (-1: library default)")
     ap.add_argument("--comm", action="store_true",
                     help="attach an RCCL communicator even at N = 1 (runs the sharded/all-reduce leg)")
     ap.add_argument("--shard", default="rows", choices=["rows", "columns"],
@@ -170,6 +172,8 @@ def measure(ctx, args, m, n_total):
     gc.set_tuning("fused", args.fused)
     gc.set_tuning("onepass", args.onepass)
     gc.set_tuning("onepass_variant", args.onepass_variant)
+    if args.onepass_cache >= 0:
+        gc.set_tuning("onepass_cache_permille", args.onepass_cache)
     # graph replay needs per-kernel events off; timing mode launches eagerly with
     # HIP events around every kernel on the solver stream.
     gc.solver_reset(b, mu, use_graph=True)

@@ -84,6 +84,7 @@ struct bpgl_ctx {
     int onepass = -1;          // tuning: -1 when eligible, 0 off, 1 required
     int op_refresh = 64;       // exact g = A^T r every this many iterations (0: at reset only)
     int op_variant = 0;        // ring depth / prefetch variant (OpVar)
+    int op_cache = 0;          // permille of each row group read with cache-allocating loads
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
     int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
@@ -695,6 +696,7 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
         c->op.R = c->op_R;
         c->op.xl = c->op_xl;
         c->op.ls = c->rows ? 0 : 1;   // row shards: the line search follows the all-reduce
+        c->op.cache_permille = c->op_cache;
     }
     HIP_TRY(hipSetDevice(c->device));
     if (c->op_shape) HIP_TRY(hipMemsetAsync(s + L.opPG, 0, 8 * c->m * c->op_SB, c->stream));   // tag 0: never written
@@ -1032,6 +1034,14 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "onepass_variant")) {
         if (value < 0 || value >= kOpVariants) return fail(BPGL_E_ARG, "onepass_variant must be in [0, %d)", kOpVariants);
         c->op_variant = (int)value;
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "onepass_cache_permille")) {
+        if (value < 0 || value > 1000) return fail(BPGL_E_ARG, "onepass_cache_permille must be in [0, 1000]");
+        c->op_cache = (int)value;
+        c->op.cache_permille = c->op_cache;
         drop_graphs(c);
         c->solver = false;
         return 0;

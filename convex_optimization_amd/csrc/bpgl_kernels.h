@@ -44,6 +44,7 @@ struct DevState {
     long long op_epoch;   // one-pass mode: launches so far (tag of the row-partial hand-off)
     long long op_fail;    // one-pass mode: a hand-off poll ran out (blocks not co-resident)
     unsigned long long op_cnt;   // one-pass mode: row-group arrivals (k_onepass line search)
+    long long op_base;    // one-pass mode: op_epoch at the solver reset (row direction = parity since)
 };
 
 struct Params {
@@ -738,6 +739,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(Params p) {
         st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0; st->pending = 0;
         st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0; st->op_fail = 0;
         st->op_cnt = 0;
+        st->op_base = st->op_epoch;
         st->t_base = (long long)wall_clock64();
         if (p.time_iter) p.time_iter[0] = 0.0;
     }

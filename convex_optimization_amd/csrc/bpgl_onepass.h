@@ -55,6 +55,7 @@ struct OnePassArgs {
     unsigned long long* PG;      // [m][SB] tagged row partials
     int SB, ngroups, R, xl;      // segment blocks per row, row groups, rows per group, XCD-local map
     int ls;                      // 1: the last row group to finish runs the line search (one rank)
+    int cache_permille;          // share of each group's rows read last with cache-allocating loads
 };
 
 typedef unsigned long long op_u64;
@@ -177,6 +178,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     else { grp = b / SB; sb = b % SB; }
     const long long i0 = (long long)grp * o.R;
     const long long i1 = i0 + o.R < p.m ? i0 + o.R : p.m;
+    // launches alternate the row direction; each reads the last cache_permille of its rows with
+    // cache-allocating loads, which the next launch (opposite direction) reads first from the
+    // Infinity Cache (only the small tail kernel runs in between)
+    const bool rev = ((p.st->op_epoch - p.st->op_base) & 1) != 0;   // per solver run: reruns repeat bits
+    auto rowof = [&](int t) -> long long { return rev ? i1 - 1 - t : i0 + t; };
     const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
     if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
         if (sb == 0 && threadIdx.x == 0) { st_sc1(p.parts2 + 2ll * grp, 0.0); st_sc1(p.parts2 + 2ll * grp + 1, 0.0); }
@@ -215,28 +221,31 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     unsigned polls = kOpPolls;
     bool failed = false;
 
-    auto load = [&](int t, int slot) {
+    const int tcache = nrows - (int)(((long long)nrows * o.cache_permille) / 1000);
+    // NTL: the load policy, a compile-time choice per copy of the row loop (a runtime branch
+    // around the loads makes the compiler drain the load queue at the join)
+    auto load = [&](auto NTL, int t, int slot) {
         const int tc = t < nrows ? t : nrows - 1;
-        const T* rp = Ab + (i0 + tc) * p.lda;
+        const T* rp = Ab + rowof(tc) * p.lda;
 #pragma unroll
-        for (int k = 0; k < LU; ++k) buf[slot][k] = ldv<T, true>(rp + col[k]);
+        for (int k = 0; k < LU; ++k) buf[slot][k] = ldv<T, decltype(NTL)::value>(rp + col[k]);
     };
     auto gload = [&](int t, int slot) {   // granules consumed at step t (phase 2 of row t - LAG)
         int t2 = t - LAG;
         t2 = t2 < 0 ? 0 : (t2 >= nrows ? nrows - 1 : t2);
 #pragma unroll
         for (int k = 0; k < GPL; ++k)
-            gv[slot][k] = __hip_atomic_load(o.PG + (i0 + t2) * SB + glane[k], __ATOMIC_RELAXED,
+            gv[slot][k] = __hip_atomic_load(o.PG + rowof(t2) * SB + glane[k], __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
     };
 
     // one row step: prefetch row t + PF (and the granules of its phase 2), phase 1 of row t,
     // publication of row t - 1, phase 2 of row t - LAG.  (A branch-free steady-state copy of
     // the loop made the register allocator spill: the three loop copies are not worth it.)
-    auto step = [&](const int q, const int t) {
+    auto step = [&](auto NTL, const int q, const int t) {
         const int qn = (q + PF) % NB;
         gload(t + PF, qn);
-        load(t + PF, qn);
+        load(NTL, t + PF, qn);
         if (t < nrows) {   // phase 1: this wave's partial of s23[t] into its LDS slot
             double acc[4] = {0.0, 0.0, 0.0, 0.0};   // 4 independent FMA chains, folded in a fixed order
 #pragma unroll
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             }
             const double bsum = op_quad_sum(op_unstuff(w));   // (p0 + p1) + (p2 + p3) in lane 0
             if (lane == 0)
-                __hip_atomic_store(o.PG + (i0 + tp) * SB + sb, op_stuff(bsum, tag), __ATOMIC_RELAXED,
+                __hip_atomic_store(o.PG + rowof(tp) * SB + sb, op_stuff(bsum, tag), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
         const int t2 = t - LAG;
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
                 return ok;
             };
             if (!__all(ready())) {   // late: re-poll (drains this wave's queue; rare)
-                const op_u64* src = o.PG + (i0 + t2) * SB;
+                const op_u64* src = o.PG + rowof(t2) * SB;
                 do {
                     if (polls == 0) { failed = true; break; }
                     --polls;
@@ -299,7 +308,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             double x = lane < SB ? op_unstuff(v[0]) : 0.0;
             if (GPL == 2) x += lane + 64 < SB ? op_unstuff(v[GPL - 1]) : 0.0;   // blocks l and l + 64, then the wave
             x = SB <= 16 ? op_lane(op_row_sum16(x), 0) : op_wave_sum(x);
-            if (sb == 0 && wave == 0 && lane == 0) o.S[i0 + t2] = x;
+            if (sb == 0 && wave == 0 && lane == 0) o.S[rowof(t2)] = x;
 #pragma unroll
             for (int k = 0; k < LU; ++k) {
                 double v2[N];
@@ -310,11 +319,19 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         }
     };
 
+    using NTon = std::integral_constant<bool, true>;
+    using NToff = std::integral_constant<bool, false>;
 #pragma unroll
-    for (int q = 0; q < PF; ++q) { gload(q, q); load(q, q); }
-    for (int base = 0; base < nrows + LAG; base += NB) {   // base stays a multiple of NB: slots are static
+    for (int q = 0; q < PF; ++q) { gload(q, q); load(NTon{}, q, q); }
+    int base = 0;   // stays a multiple of NB: ring slots are static
+    // rows issued before tcache stream non-temporally, the rest allocate in the caches
+    for (; base + NB + PF <= tcache; base += NB) {
 #pragma unroll
-        for (int q = 0; q < NB; ++q) step(q, base + q);
+        for (int q = 0; q < NB; ++q) step(NTon{}, q, base + q);
+    }
+    for (; base < nrows + LAG; base += NB) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) step(NToff{}, q, base + q);
     }
     if (failed && lane == 0) atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
     if (sb == 0 && wave == 0) {

@@ -208,6 +208,10 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
  *   one feature block, one rank (or row shards), no fused mode, at most
  *   128 x 4096 columns (fp32/bf16; 128 x 2048 for fp64) and all of its blocks
  *   resident at once (nothing else running on the device).
+ *   "onepass_cache_permille" (default 0): share of every row group the one-pass
+ *   kernel reads with cache-allocating loads (launches alternate the row
+ *   direction, so the next launch starts on those rows).
+ *   "onepass_variant" (default 0, 0-3): register-ring depth / prefetch distance.
  *   "onepass_refresh" (default 64; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "fused" (default 0): the two-launch fused iteration.
