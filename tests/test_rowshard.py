@@ -159,3 +159,42 @@ def test_row_shard_argument_errors():
     # bind already happened: the layout is fixed
     with pytest.raises(N.BpglError, match="precede"):
         N.check(N.lib().bpgl_set_shard(gc._ctx, N.BPGL_SHARD_COLUMNS), "bpgl_set_shard")
+
+
+@pytest.mark.parametrize("type_name,world", [("double", 2), ("bf16", 3)])
+def test_external_row_ranks_storage_types(type_name, world):
+    """fp64 and bf16 storage of the row shards (the bf16 case against the one-rank solver on the
+    same bf16-rounded A): every rank's x bit-identical, <= 1e-10 from one rank"""
+    rs = np.random.RandomState(30 + world)
+    m, n = 700, 9000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.2, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    ref = make_cls(type_name)(A, 1, device=0).run(b, mu, 120)
+    ranks = run_external(A, b, mu, world, 120, type_name=type_name)
+    xs = [gc.solver_x() for gc in ranks]
+    for x in xs[1:]:
+        np.testing.assert_array_equal(x, xs[0])
+    assert rel(xs[0], ref["x"]) <= 1e-10, rel(xs[0], ref["x"])
+
+
+def test_two_granules_ragged_width_with_records():
+    """SB = 97 segment blocks (w = 395000, not a multiple of the 4096-column block), err_iter /
+    time_iter recording and the err_bound rule through the one-rank RCCL row path"""
+    rs = np.random.RandomState(12)
+    m, n = 96, 395000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.05, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    plain = make_cls("float")(A, 1, device=0)
+    plain.set_tuning("onepass", 0)
+    two = plain.run(b, mu, 60, err_bound=1e-3, record=True)
+    rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    one = rows.run(b, mu, 60, err_bound=1e-3, record=True)
+    assert one["t_last"] == two["t_last"] and one["stopped"] == two["stopped"]
+    assert rel(one["x"], two["x"]) <= 1e-10, rel(one["x"], two["x"])
+    T = one["t_last"] + 1
+    np.testing.assert_allclose(one["err_iter"][:T], two["err_iter"][:T], rtol=1e-8, atol=1e-12)
+    # times of the completed iterations increase; the stopping iteration records none, as the
+    # reference breaks before time_record (lasso.py:147-157)
+    assert np.all(np.diff(one["time_iter"][:T]) > 0) and one["time_iter"][T] == 0.0
