@@ -218,7 +218,7 @@ __device__ __forceinline__ void colpass_span(const T* __restrict__ Ab, long long
 #define BPGL_STAMP 0
 #endif
 #if BPGL_STAMP
-__device__ unsigned long long g_stamps[2][2][16384];
+__device__ unsigned long long g_stamps[3][2][16384];   // [colpass, rowpass, onepass][start, end][block]
 #define BPGL_STAMP_AT(kern, se)                                                                   \
     do {                                                                                          \
         if ((se) == 1) __syncthreads();                                                           \

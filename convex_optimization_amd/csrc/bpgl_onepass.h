@@ -195,6 +195,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
 
     for (int k = threadIdx.x; k < kOpSlots * kWaves; k += kThreads) (&part[0][0])[k] = 1ull;   // rows 0..31: parity 0
     __syncthreads();
+    BPGL_STAMP_AT(2, 0);
 
     // this lane's columns: LU 16-byte groups, 64 * N apart
     const T* __restrict__ Ab = reinterpret_cast<const T*>(p.A);
@@ -333,6 +334,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
 #pragma unroll
         for (int q = 0; q < NB; ++q) step(NToff{}, q, base + q);
     }
+    BPGL_STAMP_AT(2, 1);
     if (failed && lane == 0) atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
     if (sb == 0 && wave == 0) {
         // this row group's share of the line search, r.s23 and s23.s23, from the s23 rows this

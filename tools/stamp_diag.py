@@ -30,7 +30,7 @@ def main():
     gc.solver_reset(b, mu, use_graph=False)
     gc.solver_step(5)
     gc.stream.synchronize()
-    st = np.zeros((2, 2, 16384), dtype=np.uint64)
+    st = np.zeros((3, 2, 16384), dtype=np.uint64)
     L = _native.lib()
     L.bpgl_diag_stamps.argtypes = [ctypes.c_void_p]
     assert L.bpgl_diag_stamps(st.ctypes.data_as(ctypes.c_void_p)) == 0
