@@ -53,3 +53,34 @@ def test_default_arguments_are_the_headline_config():
     assert (a.gpus, a.m, a.n_per_gpu, a.block, a.type, a.rhs) == (1, 8192, 65536, 1, "float", 1)
     assert a.onepass == -1   # the library's choice: one pass when eligible
     assert a.steps > 0 and a.warmup >= 0
+
+
+def test_multi_gpu_defaults_keep_per_gpu_bytes():
+    """N > 1: row shards by default; the weak-scaling shape (m = 8192, n = 65536 N) gives every
+    GPU exactly the bytes of A of N = 1, and the rows cover m once"""
+    b = _bench()
+    from convex_optimization_amd.distributed import row_bounds
+    import sys
+    argv = sys.argv
+    try:
+        sys.argv = ["bench.py", "--gpus", "8"]
+        a = b.parse()
+    finally:
+        sys.argv = argv
+    assert a.shard == "rows"
+    for G in (1, 2, 4, 8):
+        n = a.n_per_gpu * G
+        rows = [row_bounds(a.m, g, G) for g in range(G)]
+        assert sum(e - s for s, e in rows) == a.m
+        assert all((e - s) * n == a.m * a.n_per_gpu for s, e in rows)
+
+
+def test_emit_writes_one_json_line():
+    import io
+    import json
+    b = _bench()
+    buf = io.StringIO()
+    b._JSON_OUT = buf
+    b.emit({"metric": "m", "value": 1.0})
+    lines = buf.getvalue().splitlines()
+    assert len(lines) == 1 and json.loads(lines[0])["value"] == 1.0
