@@ -15,7 +15,8 @@ import re
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libbpgl.so")
+# BPGL_LIB: another in-tree build of the same library (diagnostic builds under build_diag/)
+LIB_PATH = os.environ.get("BPGL_LIB") or os.path.join(_HERE, "_lib", "libbpgl.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bpgl.h")
 
 BPGL_F32, BPGL_F64, BPGL_BF16 = 0, 1, 2

@@ -118,6 +118,21 @@ __device__ __forceinline__ __bf16 to_bf16(float v) { return (__bf16)v; }
 __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
     __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)lds_base, 16, 0, 0);
 }
+// cache policy of the A stream, read once per pass by one block: nt (aux 2) measured 3-8 %
+// faster per pass than the default policy (profiles/r01/sweeps/panel_policy.jsonl); the
+// k-wide operand, which every block re-reads from L2, keeps the default (BPGL_PANEL_O_AUX)
+#ifndef BPGL_PANEL_A_AUX
+#define BPGL_PANEL_A_AUX 2
+#endif
+#ifndef BPGL_PANEL_O_AUX
+#define BPGL_PANEL_O_AUX 0
+#endif
+__device__ __forceinline__ void glds16a(const void* src, char* lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)lds_base, 16, 0, BPGL_PANEL_A_AUX);
+}
+__device__ __forceinline__ void glds16o(const void* src, char* lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)lds_base, 16, 0, BPGL_PANEL_O_AUX);
+}
 // all but the youngest N vector-memory ops of this wave done, LDS reads retired, then barrier
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
@@ -142,7 +157,7 @@ __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__
     const int rr = pc * 8 + (lane >> 3);
     const int c = swz128(rr, lane & 7);
     const int hl = rr / G::K, rhs = rr % G::K;
-    glds16((hl ? lo : hi) + (long long)rhs * ld + ks + 8 * c, obuf + pc * 1024);
+    glds16o((hl ? lo : hi) + (long long)rhs * ld + ks + 8 * c, obuf + pc * 1024);
 }
 // pass-1 A stage: rows ks..ks+63 of A, columns col0..col0+255 -> [64][512 B] (a piece = 2 rows)
 template <int NT>
@@ -152,7 +167,7 @@ __device__ __forceinline__ void panel_a1_piece(int q, const __bf16* __restrict__
     const int pc = q * G::NW + wave;
     const int row = pc * 2 + (lane >> 5);
     const int c = swz512(row, lane & 31);
-    glds16(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
+    glds16a(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
 }
 // pass-2 A stage: rows r0..r0+255 of A, columns ks..ks+63 -> [256][128 B] (a piece = 8 rows)
 template <int NT>
@@ -162,7 +177,7 @@ __device__ __forceinline__ void panel_a2_piece(int q, const __bf16* __restrict__
     const int pc = q * G::NW + wave;
     const int row = pc * 8 + (lane >> 3);
     const int c = swz128(row, lane & 7);
-    glds16(A + (r0 + row) * lda + ks + 8 * c, abuf + pc * 1024);
+    glds16a(A + (r0 + row) * lda + ks + 8 * c, abuf + pc * 1024);
 }
 
 // B fragment (lane: rhs = lane & 15 of the N-tile, K = 32h + 8(lane>>4) + 0..7)
