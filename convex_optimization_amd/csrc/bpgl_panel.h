@@ -60,7 +60,7 @@ struct PanelState {
     long long t;        // next iteration
     long long iters;
     double last_err;
-    long long cur_mb;   // block of the iteration being finished (set by k_panel_step)
+    long long cur_mb;   // block of the iteration being finished (set by the line search)
     long long pad[4];
 };
 
@@ -90,6 +90,7 @@ struct PanelParams {
     double* err_iter;   // [rec_len] max over RHS per iteration (nullable)
     long long rec_len;
     PanelState* st;
+    unsigned long long* cnt;   // [k] k_panel_reduce arrivals per RHS (monotone: launch q ends at q * groups)
 };
 
 constexpr int kLspRows = 1024;    // rows per line-search partial
@@ -545,9 +546,20 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, 
         }
 }
 
+__device__ __forceinline__ void panel_st_sc1(double* q, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(q), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double panel_ld_sc1(const double* q) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(q),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool LSP_SC1> __device__ void panel_step_rhs(const PanelParams& p, int rhs);
+
 // S = sum over chunks (fp64, fixed order); line-search partials per RHS and
 // 1024-row group (mode 1), or plain output (mode 0, API).  grid = k x (m / 1024);
-// a thread owns 4 consecutive rows (16-B slab loads).
+// a thread owns 4 consecutive rows (16-B slab loads).  Mode 1: the last block of an RHS to
+// finish runs that RHS's line search (panel_step_rhs), so no separate step launch.
 __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double* __restrict__ Sout, int mode) {
     const int rhs = blockIdx.x % p.k;
     const int grp = blockIdx.x / p.k;
@@ -582,16 +594,26 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
     ss = wave_sum(ss);
     if (lane == 0) { sr[wave] = rs; sq[wave] = ss; }
     __syncthreads();
+    __shared__ int last;
     if (threadIdx.x == 0) {
         double* dst = p.lsp + ((long long)grp * p.k + rhs) * 2;
-        dst[0] = ((sr[0] + sr[1]) + sr[2]) + sr[3];
-        dst[1] = ((sq[0] + sq[1]) + sq[2]) + sq[3];
+        panel_st_sc1(dst, ((sr[0] + sr[1]) + sr[2]) + sr[3]);
+        panel_st_sc1(dst + 1, ((sq[0] + sq[1]) + sq[2]) + sq[3]);
+        const unsigned long long ng = (unsigned long long)((p.m + kLspRows - 1) / kLspRows);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long old = __hip_atomic_fetch_add(p.cnt + rhs, 1ull, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+        last = ((old + 1) % ng) == 0;
     }
+    __syncthreads();
+    if (last) panel_step_rhs<true>(p, rhs);
 }
 
-// per-RHS line search: one block per RHS
-__global__ __launch_bounds__(kThreads) void k_panel_step(PanelParams p) {
-    const int rhs = blockIdx.x;
+// per-RHS line search (lasso.py:129-136): the pass-1 norm partials and the reduce's r.s / s.s
+// partials of one RHS folded in a fixed order -> gamma, err.  LSP_SC1: read the line-search
+// partials write-through (they were written by other blocks of the running launch).
+template <bool LSP_SC1>
+__device__ void panel_step_rhs(const PanelParams& p, int rhs) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb1 = (int)(p.w / kPanelRows);
     double a = 0.0, b = 0.0, e = 0.0;
@@ -615,8 +637,9 @@ __global__ __launch_bounds__(kThreads) void k_panel_step(PanelParams p) {
         double rs = 0.0, ss = 0.0;
         const int ng = (int)((p.m + kLspRows - 1) / kLspRows);
         for (int g = 0; g < ng; ++g) {
-            rs += p.lsp[((long long)g * p.k + rhs) * 2];
-            ss += p.lsp[((long long)g * p.k + rhs) * 2 + 1];
+            const double* q = p.lsp + ((long long)g * p.k + rhs) * 2;
+            rs += LSP_SC1 ? panel_ld_sc1(q) : q[0];
+            ss += LSP_SC1 ? panel_ld_sc1(q + 1) : q[1];
         }
         const double r1 = rs + p.mu[rhs] * (a - b);
         p.gamma[rhs] = (ss == 0.0) ? 0.0 : proj(-r1 / ss, 0.0, 1.0);

@@ -18,6 +18,8 @@ using namespace bpgl_host;
 // ===========================================================================
 // panel path (k right-hand sides, bf16 A, MFMA): BASELINE configs[4]
 // ===========================================================================
+constexpr int kPanelKinds = 5;   // pass1, pass2, reduce, step, update
+
 struct bpgl_panel {
     int device = 0;
     int64_t m = 0, n = 0, w = 0;
@@ -29,14 +31,14 @@ struct bpgl_panel {
     bool timing = false;
     std::vector<hipEvent_t> evs;
     int64_t timed_iters = 0;
+    bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
     int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
 };
 
 namespace {
-constexpr int kPanelKinds = 5;   // pass1, pass2, reduce, step, update
 
 struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, total;
+    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -60,6 +62,7 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.mu = k.take(8 * c->k);
     L.gamma = k.take(8 * c->k);
     L.err_rhs = k.take(8 * c->k);
+    L.cnt = k.take(8 * c->k);
     L.total = k.off;
     return L;
 }
@@ -107,6 +110,7 @@ int panel_reduce(bpgl_panel* c, double* out, int mode) {
 }
 void panel_ev(bpgl_panel* c, int64_t it, int kind, int end) {
     if (!c->timing) return;
+    c->kind_used[kind] = true;
     const size_t idx = 2 * ((size_t)it * kPanelKinds + kind) + end;
     while (c->evs.size() <= idx) {
         hipEvent_t e;
@@ -124,12 +128,8 @@ int panel_iteration(bpgl_panel* c, int64_t it) {
     if ((rc = panel_launch(c, 1, -1, nullptr, 1))) return rc;
     panel_ev(c, it, 1, 1);
     panel_ev(c, it, 2, 0);
-    if ((rc = panel_reduce(c, c->p.S, 1))) return rc;
+    if ((rc = panel_reduce(c, c->p.S, 1))) return rc;   // its last block per RHS runs the line search
     panel_ev(c, it, 2, 1);
-    panel_ev(c, it, 3, 0);
-    hipLaunchKernelGGL(k_panel_step, dim3((unsigned)c->k), dim3(kThreads), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_panel_step");
-    panel_ev(c, it, 3, 1);
     panel_ev(c, it, 4, 0);
     const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
     hipLaunchKernelGGL(k_panel_update, dim3((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192)), dim3(kThreads), 0,
@@ -242,6 +242,7 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.mu = (const double*)(s + L.mu);
     p.gamma = (double*)(s + L.gamma);
     p.err_rhs = (double*)(s + L.err_rhs);
+    p.cnt = (unsigned long long*)(s + L.cnt);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
     c->bound = true;
@@ -369,6 +370,7 @@ int bpgl_panel_kernel_times(bpgl_panel* c, double* avg_ms /* 5 */, int64_t* samp
     double sum[kPanelKinds] = {0};
     for (int64_t it = 0; it < c->timed_iters; ++it)
         for (int k = 0; k < kPanelKinds; ++k) {
+            if (!c->kind_used[k]) continue;
             const size_t i0 = 2 * ((size_t)it * kPanelKinds + k);
             float ms = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms, c->evs[i0], c->evs[i0 + 1]));
@@ -377,6 +379,7 @@ int bpgl_panel_kernel_times(bpgl_panel* c, double* avg_ms /* 5 */, int64_t* samp
     for (int k = 0; k < kPanelKinds; ++k) avg_ms[k] = c->timed_iters ? sum[k] / c->timed_iters : 0.0;
     if (samples) *samples = c->timed_iters;
     c->timed_iters = 0;
+    for (int k = 0; k < kPanelKinds; ++k) c->kind_used[k] = false;
     return 0;
 }
 

@@ -251,7 +251,7 @@ int bpgl_panel_step(bpgl_panel* ctx, int64_t n_iter);
 int bpgl_panel_status(bpgl_panel* ctx, int64_t* iters, double* last_err);
 const float* bpgl_panel_x(bpgl_panel* ctx);
 int bpgl_panel_set_kernel_timing(bpgl_panel* ctx, int enable);
-int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce, step, update */,
+int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce (+ line search), step (0: folded into reduce), update */,
                             int64_t* samples);
 /* tuning knobs (results are bitwise independent of them): "interleave1",
  * "interleave2" (pass 1 / pass 2; "interleave" sets both) 0/1/2 -- LDS-DMA
