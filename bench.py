@@ -73,7 +73,9 @@ def parse():
                     help="BASELINE.json configs[K]: 1 = 8192x65536 fp32 (default), 2 = its column-sharded "
                          "multi-GPU form, 3 = 1048576x4096 fp32, 4 = k=128 right-hand sides on bf16 A")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=256,
+                    help="timed iterations (default 256: with the default warmup the window holds exactly one "
+                         "exact-gradient refresh of the one-pass iteration, i.e. its amortised cost)")
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--m", type=int, default=M)
     ap.add_argument("--n-per-gpu", type=int, default=N_PER_GPU)
@@ -449,7 +451,7 @@ def main():
             "parallelism": f"{'row' if rows else 'column'}-shard x{G}", "rccl": bool(G > 1 or args.comm),
             "global_iters_per_s": iters_s_graph,
             "iteration": ("one pass over A (k_onepass: s23 = A D and U = A^T s23 together; g += gamma U, "
-                          "exact g = A^T r every 64 iterations)" + (
+                          "exact g = A^T r every 256 iterations)" + (
                               "; row shards: k_onepass_fold + RCCL all-reduce of [U | r.s23 | s23.s23]"
                               if rows and G > 1 else "") if onepass else
                           "two passes over A (A^T r, then A D)"),

@@ -82,7 +82,12 @@ struct bpgl_ctx {
     // one-pass iteration (bpgl_onepass.h)
     int cus = 256;
     int onepass = -1;          // tuning: -1 when eligible, 0 off, 1 required
-    int op_refresh = 64;       // exact g = A^T r every this many iterations (0: at reset only)
+    // exact g = A^T r every this many iterations (0: at reset only).  The recurrence's own drift is
+    // below the trajectory's rounding sensitivity: after 1024 iterations at configs[1], x is within
+    // 1-2e-7 of the two-pass iterates for periods 0, 64, 256 and 1024 alike, the objective within
+    // 3e-15 (profiles/r01/sweeps/onepass_refresh_drift.jsonl); 256 keeps the refresh (one A^T r pass)
+    // at 0.4 % of the iteration time
+    int op_refresh = 256;
     int op_variant = 0;        // ring depth / prefetch variant (OpVar)
     int op_cache = 0;          // permille of each row group read with cache-allocating loads
     bool op_shape = false;     // the shape admits it (geometry)

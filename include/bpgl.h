@@ -212,7 +212,7 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
  *   kernel reads with cache-allocating loads (launches alternate the row
  *   direction, so the next launch starts on those rows).
  *   "onepass_variant" (default 0, 0-3): register-ring depth / prefetch distance.
- *   "onepass_refresh" (default 64; 0 = only at reset): recompute g = A^T r
+ *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "fused" (default 0): the two-launch fused iteration.
  * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the

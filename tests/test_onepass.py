@@ -2,7 +2,7 @@
 carried as g += gamma A^T (A D).  Same algorithm as the two-pass iteration
 (lasso.py:102-157); the arithmetic differs by summation order, by <= 1 ulp per hand-off
 partial (the parity bit) and by the recurrence's accumulated rounding between exact
-refreshes (every 64 iterations by default).  Tolerances, relative l2 on x:
+refreshes (every 256 iterations by default).  Tolerances, relative l2 on x:
   * a few iterations: <= 1e-12 against the two-pass path (measured ~1e-15);
   * 25 iterations of random problems: <= 1e-8 (measured 1e-15 .. 3e-9: these lasso
     trajectories amplify rounding -- the two-pass path itself drifts 6e-10 from the
@@ -111,6 +111,7 @@ def test_graph_eager_split_steps_bitwise():
     c = gc.run(b, mu, 90, use_graph=True)["x"]
     np.testing.assert_array_equal(a, e)
     np.testing.assert_array_equal(a, c)
+    gc.set_tuning("onepass_refresh", 64)
     gc.solver_reset(b, mu)
     for k in (3, 17, 8, 62):   # crosses the refresh points 64 and 0 in different graph phases
         gc.solver_step(k)
