@@ -158,19 +158,37 @@ class GPU_Calculation:
         return dict(nseg=v[0].value, nchunk=v[1].value, rows_per_chunk=v[2].value, seg_width=v[3].value)
 
     # -- GEMV entry points ----------------------------------------------------
+    def _pinned(self, key, n):
+        """Page-locked host staging buffer (fp64, >= n values) for the host-array GEMV calls of the
+        reference's hybrid drivers: DMA straight from/to it instead of a pageable bounce."""
+        buf = self.__dict__.setdefault("_pin", {}).get(key)
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(n, dtype=torch.float64).pin_memory()
+            self._pin[key] = buf
+        return buf[:n]
+
     def _stage_in(self, v, dst, n):
         if isinstance(v, torch.Tensor):
             dst[:n].copy_(v.reshape(-1)[:n].to(dtype=torch.float64), non_blocking=True)
         else:
-            a = np.ascontiguousarray(np.asarray(v, dtype=np.float64).reshape(-1)[:n])
-            dst[:n].copy_(torch.from_numpy(a), non_blocking=False)
+            a = np.asarray(v, dtype=np.float64).reshape(-1)[:n]
+            pin = self._pinned("in%d" % dst.numel(), n)
+            # the previous copy out of this buffer must have finished before it is overwritten
+            if getattr(self, "_pin_in_event", None) is not None:
+                self._pin_in_event.synchronize()
+            pin.numpy()[...] = a
+            dst[:n].copy_(pin, non_blocking=True)
+            self._pin_in_event = torch.cuda.Event()
+            self._pin_in_event.record(torch.cuda.current_stream(self.device))
 
-    @staticmethod
-    def _stage_out(src, out):
+    def _stage_out(self, src, out):
         if isinstance(out, torch.Tensor):
             out.view(-1).copy_(src.to(dtype=out.dtype))
         else:
-            out[...] = src.cpu().numpy().reshape(out.shape)
+            pin = self._pinned("out%d" % src.numel(), src.numel())
+            pin.copy_(src, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            out[...] = pin.numpy().reshape(out.shape)
 
     def mat_tMulVec_DiffSize(self, s13, index_m, s11):
         """s13 <- A_m^T s11 (gpu_calculation.py:264-277)."""
