@@ -126,7 +126,7 @@ void geometry(bpgl_ctx* c) {
     c->nparts = (int)cdiv(c->wp, kColsPerShrink);
     // one-pass geometry: SB segment blocks per row, floor(CUs / SB) row groups, one block per CU
     const int bc = c->dtype == BPGL_F32 ? OnePassGeo<4, float>::BC
-                 : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<2, bf16_t>::BC;
+                 : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<3, bf16_t>::BC;
     const int64_t SB = cdiv(c->wp, bc);
     c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
     c->op_gpl = SB > 64 ? 2 : 1;
@@ -268,20 +268,22 @@ int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) { return r
 // one-pass iteration (bpgl_onepass.h)
 // ---------------------------------------------------------------------------
 // ring slots NB and rows in flight PF per variant (tuning key "onepass_variant"); the loads
-// per lane and row (LU: 4 KiB of fp32 / fp64, 2 KiB of bf16 A per wave and row) are fixed per
-// storage type because they set the geometry.  profiles/r01/sweeps/onepass6_probe.jsonl,
-// onepass_variants.jsonl
+// per lane and row (LU: 4 KiB of fp32 / fp64, 3 KiB of bf16 A per wave and row) are fixed per
+// storage type because they set the geometry.  bf16 takes LU 3: its per-row instruction path
+// (the same 16-24 fp64 FMAs and wave sums as fp32) limits it at LU 2 (2.9k it/s), LU 4 spills;
+// LU 3 with a 12-row ring reaches 3.4-3.5k it/s at configs[1]'s shape.
+// profiles/r01/sweeps/onepass6_probe.jsonl, onepass_bf16_lu3_variants.jsonl
 template <typename T> struct OpLU { static constexpr int LU = 4; };
-template <> struct OpLU<bf16_t> { static constexpr int LU = 2; };
+template <> struct OpLU<bf16_t> { static constexpr int LU = 3; };
 template <typename T, int V> struct OpVar;
 template <typename T> struct OpVar<T, 0> { static constexpr int NB = 16, PF = 3; };
 template <typename T> struct OpVar<T, 1> { static constexpr int NB = 18, PF = 4; };
 template <typename T> struct OpVar<T, 2> { static constexpr int NB = 14, PF = 3; };
 template <typename T> struct OpVar<T, 3> { static constexpr int NB = 17, PF = 4; };
-template <> struct OpVar<bf16_t, 0> { static constexpr int NB = 20, PF = 6; };
-template <> struct OpVar<bf16_t, 1> { static constexpr int NB = 24, PF = 4; };
-template <> struct OpVar<bf16_t, 2> { static constexpr int NB = 22, PF = 6; };
-template <> struct OpVar<bf16_t, 3> { static constexpr int NB = 18, PF = 6; };
+template <> struct OpVar<bf16_t, 0> { static constexpr int NB = 12, PF = 2; };
+template <> struct OpVar<bf16_t, 1> { static constexpr int NB = 10, PF = 2; };
+template <> struct OpVar<bf16_t, 2> { static constexpr int NB = 11, PF = 2; };
+template <> struct OpVar<bf16_t, 3> { static constexpr int NB = 9, PF = 2; };
 constexpr int kOpVariants = 4;
 
 // the two-pass kernels' view of one-pass state: g is read from G (one slab row), s23 from S

@@ -206,8 +206,8 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
  *   "onepass" (default -1 = when eligible, 0 = off, 1 = required): one pass
  *   over A per iteration, the gradient carried as g += gamma A^T (A D); needs
  *   one feature block, one rank (or row shards), no fused mode, at most
- *   128 x 4096 columns (fp32/bf16; 128 x 2048 for fp64) and all of its blocks
- *   resident at once (nothing else running on the device).
+ *   128 x 4096 columns (fp32; 128 x 6144 for bf16, 128 x 2048 for fp64) and all
+ *   of its blocks resident at once (nothing else running on the device).
  *   "onepass_cache_permille" (default 0): share of every row group the one-pass
  *   kernel reads with cache-allocating loads (launches alternate the row
  *   direction, so the next launch starts on those rows).
