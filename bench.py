@@ -101,6 +101,9 @@ def parse():
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
     ap.add_argument("--interleave", type=int, default=-1,
                     help="panel path mainloop variant 0/1/2 for both passes (-1: library defaults)")
+    ap.add_argument("--d-split", type=int, default=-1, choices=[-1, 1, 2],
+                    help="panel path: the direction enters the A D pass as a hi + lo bf16 pair (2) or as its "
+                         "bf16 rounding (1); -1: library default")
     a = ap.parse_args()
     if a.config == 3:
         a.m, a.n_per_gpu = 1048576, 4096
@@ -311,6 +314,9 @@ def main_panel(args):
     pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks)
     if args.interleave >= 0:
         pl.set_tuning("interleave", args.interleave)
+    if args.d_split > 0:
+        pl.set_tuning("d_split", args.d_split)
+    d_split = pl.get_tuning("d_split")
     del A
     Ab = pl.A_bf16.float()
     B = (Ab @ Xt + 0.01 * torch.randn(m, k, device="cuda", generator=g)).double()
@@ -339,7 +345,9 @@ def main_panel(args):
     dom = max(("pass1_mfma", "pass2_mfma"), key=lambda q: kms[q])
     pb = panel_bytes_pass(m, w, k)
     achieved = pb / (kms[dom] * 1e-3) / 1e9
-    flops = 2 * m * w * k * 2                                    # hi + lo operand halves
+    # MFMA work of the dominant pass: the residual always enters as hi + lo, the direction
+    # as hi + lo (d_split 2) or hi alone (d_split 1)
+    flops = 2 * m * w * k * (2 if dom == "pass1_mfma" else d_split)
     tflops = flops / (kms[dom] * 1e-3) / 1e12
     iters_s = args.steps / el_graph
     alg_iter = 2 * m * w * 2 + 4 * k * 5 * (w + m)          # SURVEY.md 8d (c5: 2.336e9 B -> 3425 it/s)
@@ -348,12 +356,14 @@ def main_panel(args):
         "value": iters_s, "unit": f"iters/s ({k} right-hand sides per iteration)",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el_graph / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16 (A) x split-bf16 operands, fp32 MFMA accumulate, fp64 reduce",
+        "vs_baseline": None,
+        "dtype": "bf16 (A) x hi+lo bf16 residual x " + ("hi+lo bf16" if d_split == 2 else "bf16") +
+                 " direction, fp32 MFMA accumulate, fp64 reduce",
         "data": "synthetic (A ~ N(0,1) rows unit-norm, bf16 in HBM; X_true density 0.4; B = A X_true + 0.01 E)",
         "config": {
             "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
-            "interleave": args.interleave,
+            "interleave": args.interleave, "d_split": d_split,
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
             "iter_roofline_frac": iters_s * alg_iter / (HBM_PEAK_GBS * 1e9),

@@ -10,11 +10,13 @@
 //   x_j += gamma_j D_j ;  Ax_j += gamma_j S_j ;  R = sum_b Ax_b - B
 //
 // Operands.  A is resident once, row-major bf16; every A byte is read once per
-// pass.  R and D enter the MFMA as hi + lo bf16 pairs (a ~16-bit mantissa); the direction actually used
-// is D' = Dh + Dl, with S = A D' and |x + D'|_1 in the line search, so the exact
-// line search of the reference still guarantees descent.  Accumulation: fp32
-// inside a block's MFMA chain, fp64 across pass-2 column chunks and in every
-// reduction after that.
+// pass.  R enters the MFMA as a hi + lo bf16 pair (a ~16-bit mantissa).  The
+// direction enters as the same pair (NS = 2) or as its bf16 rounding alone
+// (NS = 1, the solver's "d_split" knob): either way the direction actually used
+// is the D' the MFMA sees, with S = A D' and |x + D'|_1 in the line search, so the
+// exact line search of the reference is exact along the direction taken and
+// still guarantees descent.  Accumulation: fp32 inside a block's MFMA chain, fp64
+// across pass-2 column chunks and in every reduction after that.
 //
 // Tiles.  A block owns 256 output rows x all k RHS: 4 (M) x WN (N) waves, each
 // 64 rows (4 MFMA M-tiles) x k/WN RHS.  K advances 64 per stage.  Both operand
@@ -41,16 +43,17 @@ constexpr int kPanelNA = 3;       // A-side stage buffers (two stages in flight)
 constexpr int kPanelNO = 2;       // k-wide-side stage buffers
 constexpr int kPanelAStage = kPanelRows * kPanelK * 2;   // 32 KiB
 
-template <int NT>
+// NS: bf16 pieces of the k-wide operand (2: hi + lo, ~16-bit mantissa; 1: hi only)
+template <int NT, int NS = 2>
 struct PanelGeo {
     static constexpr int WN = NT >= 2 ? 2 : 1;        // waves along the RHS
     static constexpr int NTW = NT / WN;               // N-tiles per wave
     static constexpr int NW = 4 * WN;                 // waves per block
     static constexpr int T = 64 * NW;                 // threads per block
     static constexpr int K = 16 * NT;                 // right-hand sides
-    static constexpr int OStage = 2 * K * kPanelK * 2;            // hi + lo rows of 128 B
+    static constexpr int OStage = NS * K * kPanelK * 2;           // NS rows of 128 B per RHS
     static constexpr int LA = kPanelAStage / (T * 16);            // LDS-DMA per thread per A stage
-    static constexpr int LO = OStage / (T * 16);                  // ... per k-wide stage
+    static constexpr int LO = (OStage + T * 16 - 1) / (T * 16);   // ... per k-wide stage (a wave may idle)
     static constexpr int Smem = kPanelNA * kPanelAStage + kPanelNO * OStage;
     static_assert(LA >= 1 && LO >= 1, "stage must cover every thread");
     static_assert(Smem <= 160 * 1024, "LDS budget");
@@ -148,13 +151,16 @@ __device__ __forceinline__ int swz128(int r, int c) { return c ^ ((r >> 1) & 7);
 // 8 distinct 32-B bank groups.
 __device__ __forceinline__ int swz512(int r, int c) { return c ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2))); }
 
-// k-wide operand stage: [hl][k][64] bf16 from hi/lo [k][ld] at column ks, piece q of this
-// wave (a piece = 8 image rows of 128 B)
-template <int NT>
+// k-wide operand stage: [hl < NS][k][64] bf16 from hi/lo [k][ld] at column ks, piece q of
+// this wave (a piece = 8 image rows of 128 B).  When the stage has fewer pieces than waves
+// (NS = 1 at k = 16 or 32) the spare waves issue nothing: the stage's counted wait only
+// assumes that a wave's A pieces are its youngest operations, which still holds.
+template <int NT, int NS>
 __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__ hi, const __bf16* __restrict__ lo,
                                                long long ld, long long ks, char* obuf, int wave, int lane) {
-    using G = PanelGeo<NT>;
+    using G = PanelGeo<NT, NS>;
     const int pc = q * G::NW + wave;
+    if (pc * 8 >= NS * G::K) return;   // wave-uniform
     const int rr = pc * 8 + (lane >> 3);
     const int c = swz128(rr, lane & 7);
     const int hl = rr / G::K, rhs = rr % G::K;
@@ -208,16 +214,16 @@ __device__ __forceinline__ bf16x8 panel_afrag1(const char* abuf, int j0, int h, 
 
 // Block-tile GEMM over nsteps stages of 64:
 //   PASS 1: acc[mt][nt] += A[ks.., col0 + j]^T (Rh + Rl)[rhs][ks..]      (rows j, K = A rows)
-//   PASS 2: acc[mt][nt] += A[r0 + i][colk + ks..] (Dh + Dl)[rhs][ks..]   (rows i, K = A columns)
+//   PASS 2: acc[mt][nt] += A[r0 + i][colk + ks..] (Dh [+ Dl])[rhs][ks..] (rows i, K = A columns)
 // `a_row0`/`a_col0`: PASS 1 -> (first A row of K, first column of the tile); PASS 2 -> (first row, first column of K).
 // ILV 0: a stage's LDS-DMA pieces are issued together after the barrier; ILV 1: they
-// are spread over the stage's MFMA groups (one scheduling group each).
-template <int NT, int PASS, int ILV>
+// are spread over the stage's MFMA groups (one scheduling group each).  NS: operand pieces.
+template <int NT, int PASS, int ILV, int NS>
 __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restrict__ A, long long lda,
                                                long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
                                                const __bf16* __restrict__ bl, long long ldb, long long b_k0,
                                                int nsteps, f32x4 (&acc)[4][PanelGeo<NT>::NTW]) {
-    using G = PanelGeo<NT>;
+    using G = PanelGeo<NT, NS>;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
@@ -234,7 +240,8 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
-            panel_op_piece<NT>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave, lane);
+            panel_op_piece<NT, NS>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
+                                   lane);
         } else if (PASS == 1) {
             panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
                                abufs + ba * kPanelAStage, wave, lane);
@@ -288,15 +295,17 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
                 }
                 const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
                 const bf16x8 b_hi = panel_bfrag(ob, rhs, h, lane);
-                const bf16x8 b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
+                bf16x8 b_lo;
+                if constexpr (NS == 2) b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
 #pragma unroll
                 for (int mt = 0; mt < 4; ++mt) {
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
+                    if constexpr (NS == 2)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
                 }
                 if constexpr (ILV) {
                     if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x8, 4 * NS, 0);
                 }
             });
         });
@@ -311,13 +320,13 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 // reuse is unchanged (a stage's buffers are refilled only after the barrier that follows
 // all of its reads); all LDS-DMA pieces of a stage are issued before its barrier, spread
 // over the first G - 1 groups.
-template <int NT, int PASS>
+template <int NT, int PASS, int NS>
 __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __restrict__ A, long long lda,
                                                     long long a_row0, long long a_col0,
                                                     const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
                                                     long long ldb, long long b_k0, int nsteps,
                                                     f32x4 (&acc)[4][PanelGeo<NT>::NTW]) {
-    using G = PanelGeo<NT>;
+    using G = PanelGeo<NT, NS>;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
@@ -331,7 +340,8 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
-            panel_op_piece<NT>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave, lane);
+            panel_op_piece<NT, NS>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
+                                   lane);
         } else if (PASS == 1) {
             panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
                                abufs + ba * kPanelAStage, wave, lane);
@@ -353,7 +363,7 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
     auto read_b = [&](const char* ob, int h, int nt, bf16x8& bhi, bf16x8& blo) {
         const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
         bhi = panel_bfrag(ob, rhs, h, lane);
-        blo = panel_bfrag(ob, G::K + rhs, h, lane);
+        if constexpr (NS == 2) blo = panel_bfrag(ob, G::K + rhs, h, lane);
     };
 
     // prologue: op(0), A(0), A(1), then stage 0 landed and group 0's fragments read
@@ -395,7 +405,8 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][0], acc[mt][nt], 0, 0, 0);
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][1], acc[mt][nt], 0, 0, 0);
+                if constexpr (NS == 2)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][1], acc[mt][nt], 0, 0, 0);
             }
         });
         abuf = abuf_next;
@@ -411,9 +422,10 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 
 // ---------------------------------------------------------------------------
 // pass 1: G = A_m^T R (EPI 0: write G [k][w] fp64 -- API), or the fused shrink
-// epilogue (EPI 1: D' split, norms per RHS).  grid = w / 256 blocks.
+// epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
+// per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI, int ILV>
+template <int NT, int EPI, int ILV, int DS>
 __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, int fixed_block,
                                                                   double* __restrict__ Gout) {
     using G = PanelGeo<NT>;
@@ -425,11 +437,11 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
     if constexpr (ILV == 2)
-        panel_mainloop_pipe<NT, 1>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
-                                   (int)(p.m / kPanelK), acc);
+        panel_mainloop_pipe<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+                                      (int)(p.m / kPanelK), acc);
     else
-        panel_mainloop<NT, 1, ILV>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
-                                   (int)(p.m / kPanelK), acc);
+        panel_mainloop<NT, 1, ILV, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+                                      (int)(p.m / kPanelK), acc);
 
     // C layout: row = (lane>>4)*4 + r (A column), col = lane & 15 (RHS)
     if (EPI == 0) {
@@ -463,8 +475,14 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
                 const double x = (double)xs[r];
                 const long long kx = (long long)mb * p.w + j + r;
                 const double bx = p.rec[kx] * soft_thr(p.diag[kx] * x - g, mu);
-                split_bf16(bx - x, dh[r], dl[r]);
-                const double dprime = (double)(float)dh[r] + (double)(float)dl[r];
+                double dprime;
+                if constexpr (DS == 2) {
+                    split_bf16(bx - x, dh[r], dl[r]);
+                    dprime = (double)(float)dh[r] + (double)(float)dl[r];
+                } else {
+                    dh[r] = to_bf16((float)(bx - x));
+                    dprime = (double)(float)dh[r];
+                }
                 sbx += fabs(x + dprime);
                 sx += fabs(x);
                 const double e = fabs(g - proj(g - x, -mu, mu));
@@ -472,7 +490,8 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
             }
             typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
             *reinterpret_cast<bf16x4*>(p.Dh + (long long)rhs * p.w + j) = bf16x4{dh[0], dh[1], dh[2], dh[3]};
-            *reinterpret_cast<bf16x4*>(p.Dl + (long long)rhs * p.w + j) = bf16x4{dl[0], dl[1], dl[2], dl[3]};
+            if constexpr (DS == 2)
+                *reinterpret_cast<bf16x4*>(p.Dl + (long long)rhs * p.w + j) = bf16x4{dl[0], dl[1], dl[2], dl[3]};
         }
         // lanes l, l^16, l^32, l^48 share the RHS
         sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
@@ -501,12 +520,12 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
 }
 
 // ---------------------------------------------------------------------------
-// pass 2: partial S over one column chunk: Sslab[chunk][rhs][row]
-// grid = (m / 256) x kchunks
+// pass 2: partial S over one column chunk: Sslab[chunk][rhs][row]; the direction in NS
+// bf16 pieces.  grid = (m / 256) x kchunks
 // ---------------------------------------------------------------------------
-template <int NT, int ILV>
+template <int NT, int ILV, int NS>
 __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, int fixed_block) {
-    using G = PanelGeo<NT>;
+    using G = PanelGeo<NT, NS>;
     __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
     const int lane = threadIdx.x & 63;
@@ -529,11 +548,11 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, 
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
     if constexpr (ILV == 2)
-        panel_mainloop_pipe<NT, 2>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
-                                   chunk * kc, (int)(kc / kPanelK), acc);
+        panel_mainloop_pipe<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
+                                       chunk * kc, (int)(kc / kPanelK), acc);
     else
-        panel_mainloop<NT, 2, ILV>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
-                                   chunk * kc, (int)(kc / kPanelK), acc);
+        panel_mainloop<NT, 2, ILV, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
+                                       chunk * kc, (int)(kc / kPanelK), acc);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -649,9 +668,10 @@ __device__ void panel_step_rhs(const PanelParams& p, int rhs) {
 }
 
 // x_j += gamma_j D'_j ; Ax_j += gamma_j S_j ; R = sum_b Ax_b - B ; split R.
-// Work units: u < ux -> 8 consecutive x elements ([k][w], 16-B hi/lo loads); ux <= u <
-// ux + ur -> 4 consecutive residual rows ([k][m]).  Also bumps t.  k*w and k*m < 2^31
-// (checked at create), so the index math is 32-bit.
+// Work units: u < ux -> 8 consecutive x elements ([k][w], 16-B Dh (+ Dl when DS = 2) loads);
+// ux <= u < ux + ur -> 4 consecutive residual rows ([k][m]).  Also bumps t.  k*w and k*m <
+// 2^31 (checked at create), so the index math is 32-bit.
+template <int DS>
 __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
     const int mb = (int)p.st->cur_mb;   // p.st->t is advanced by block 0 of this launch
     const long long nx = (long long)p.k * p.w, nr = (long long)p.k * p.m;
@@ -665,14 +685,18 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
             const long long e = 8ll * u;
             const double g = p.gamma[u / w8];
             const bf16x8v dh = *reinterpret_cast<const bf16x8v*>(p.Dh + e);
-            const bf16x8v dl = *reinterpret_cast<const bf16x8v*>(p.Dl + e);
+            bf16x8v dl;
+            if constexpr (DS == 2) dl = *reinterpret_cast<const bf16x8v*>(p.Dl + e);
             float* xp = p.X + (long long)mb * nx + e;
             float4 x0 = *reinterpret_cast<const float4*>(xp);
             float4 x1 = *reinterpret_cast<const float4*>(xp + 4);
             float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                xs[q] = (float)((double)xs[q] + g * ((double)(float)dh[q] + (double)(float)dl[q]));
+            for (int q = 0; q < 8; ++q) {
+                double dq = (double)(float)dh[q];
+                if constexpr (DS == 2) dq += (double)(float)dl[q];
+                xs[q] = (float)((double)xs[q] + g * dq);
+            }
             *reinterpret_cast<float4*>(xp) = make_float4(xs[0], xs[1], xs[2], xs[3]);
             *reinterpret_cast<float4*>(xp + 4) = make_float4(xs[4], xs[5], xs[6], xs[7]);
         }

@@ -33,6 +33,7 @@ struct bpgl_panel {
     int64_t timed_iters = 0;
     bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
     int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
+    int dsplit = 2;               // bf16 pieces of the solver's direction (d_split knob)
 };
 
 namespace {
@@ -67,40 +68,46 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     return L;
 }
 
-template <int NT, int ILV>
+// ns: bf16 pieces of the direction (pass 1's epilogue writes it, pass 2 reads it): the
+// solver's d_split knob, 2 for the API products (bpgl_panel_mtm / _mm)
+template <int NT, int ILV, int NS>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    const dim3 b(PanelGeo<NT>::T);
     switch (which) {
         case 0:
-            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV>), dim3((unsigned)(c->w / kPanelRows)), b, 0,
-                                         c->stream, c->p, fixed_block, out);
-            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV>), dim3((unsigned)(c->w / kPanelRows)), b, 0,
-                                    c->stream, c->p, fixed_block, out);
+            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS>), dim3((unsigned)(c->w / kPanelRows)),
+                                         dim3(PanelGeo<NT>::T), 0, c->stream, c->p, fixed_block, out);
+            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2>), dim3((unsigned)(c->w / kPanelRows)),
+                                    dim3(PanelGeo<NT>::T), 0, c->stream, c->p, fixed_block, out);
             LAUNCH_CHECK("k_panel_pass1");
             break;
         case 1:
-            hipLaunchKernelGGL((k_panel_pass2<NT, ILV>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)), b, 0,
-                               c->stream, c->p, fixed_block);
+            hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
+                               dim3(PanelGeo<NT, NS>::T), 0, c->stream, c->p, fixed_block);
             LAUNCH_CHECK("k_panel_pass2");
             break;
     }
     return 0;
 }
-template <int NT>
+template <int NT, int NS>
 int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (c->interleave[which]) {
-        case 0: return panel_launch_nt<NT, 0>(c, which, fixed_block, out, mode);
-        case 1: return panel_launch_nt<NT, 1>(c, which, fixed_block, out, mode);
-        default: return panel_launch_nt<NT, 2>(c, which, fixed_block, out, mode);
+        case 0: return panel_launch_nt<NT, 0, NS>(c, which, fixed_block, out, mode);
+        case 1: return panel_launch_nt<NT, 1, NS>(c, which, fixed_block, out, mode);
+        default: return panel_launch_nt<NT, 2, NS>(c, which, fixed_block, out, mode);
     }
 }
-int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
+template <int NS>
+int panel_launch_ns(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (c->k) {
-        case 16: return panel_launch_ilv<1>(c, which, fixed_block, out, mode);
-        case 32: return panel_launch_ilv<2>(c, which, fixed_block, out, mode);
-        case 64: return panel_launch_ilv<4>(c, which, fixed_block, out, mode);
-        default: return panel_launch_ilv<8>(c, which, fixed_block, out, mode);
+        case 16: return panel_launch_ilv<1, NS>(c, which, fixed_block, out, mode);
+        case 32: return panel_launch_ilv<2, NS>(c, which, fixed_block, out, mode);
+        case 64: return panel_launch_ilv<4, NS>(c, which, fixed_block, out, mode);
+        default: return panel_launch_ilv<8, NS>(c, which, fixed_block, out, mode);
     }
+}
+int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mode, int ns) {
+    return ns == 1 ? panel_launch_ns<1>(c, which, fixed_block, out, mode)
+                   : panel_launch_ns<2>(c, which, fixed_block, out, mode);
 }
 int panel_reduce(bpgl_panel* c, double* out, int mode) {
     hipLaunchKernelGGL(k_panel_reduce, dim3((unsigned)(c->k * cdiv(c->m, kLspRows))), dim3(kThreads), 0, c->stream,
@@ -122,18 +129,19 @@ void panel_ev(bpgl_panel* c, int64_t it, int kind, int end) {
 int panel_iteration(bpgl_panel* c, int64_t it) {
     int rc;
     panel_ev(c, it, 0, 0);
-    if ((rc = panel_launch(c, 0, -1, nullptr, 1))) return rc;
+    if ((rc = panel_launch(c, 0, -1, nullptr, 1, c->dsplit))) return rc;
     panel_ev(c, it, 0, 1);
     panel_ev(c, it, 1, 0);
-    if ((rc = panel_launch(c, 1, -1, nullptr, 1))) return rc;
+    if ((rc = panel_launch(c, 1, -1, nullptr, 1, c->dsplit))) return rc;
     panel_ev(c, it, 1, 1);
     panel_ev(c, it, 2, 0);
     if ((rc = panel_reduce(c, c->p.S, 1))) return rc;   // its last block per RHS runs the line search
     panel_ev(c, it, 2, 1);
     panel_ev(c, it, 4, 0);
     const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
-    hipLaunchKernelGGL(k_panel_update, dim3((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192)), dim3(kThreads), 0,
-                       c->stream, c->p);
+    const dim3 ug((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192));
+    if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_update<1>, ug, dim3(kThreads), 0, c->stream, c->p);
+    else hipLaunchKernelGGL(k_panel_update<2>, ug, dim3(kThreads), 0, c->stream, c->p);
     LAUNCH_CHECK("k_panel_update");
     panel_ev(c, it, 4, 1);
     return 0;
@@ -272,7 +280,7 @@ int bpgl_panel_mtm(bpgl_panel* c, int32_t block, const double* R, double* G) {
     HIP_TRY(hipSetDevice(c->device));
     if ((rc = panel_split(c, R, (int64_t)c->k * c->m, c->p.Rh, c->p.Rl, 1.0, nullptr))) return rc;
     c->solver = false;   // Rh/Rl now hold the caller's operand
-    return panel_launch(c, 0, block, G, 0);
+    return panel_launch(c, 0, block, G, 0, 2);
 }
 
 int bpgl_panel_mm(bpgl_panel* c, int32_t block, const double* D, double* S) {
@@ -283,7 +291,7 @@ int bpgl_panel_mm(bpgl_panel* c, int32_t block, const double* D, double* S) {
     HIP_TRY(hipSetDevice(c->device));
     if ((rc = panel_split(c, D, (int64_t)c->k * c->w, c->p.Dh, c->p.Dl, 1.0, nullptr))) return rc;
     c->solver = false;
-    if ((rc = panel_launch(c, 1, block, nullptr, 0))) return rc;
+    if ((rc = panel_launch(c, 1, block, nullptr, 0, 2))) return rc;
     return panel_reduce(c, S, 0);
 }
 
@@ -390,10 +398,22 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
         if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
+    } else if (!strcmp(key, "d_split")) {
+        if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
+        c->dsplit = (int)value;
     } else {
         return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     }
     if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    return 0;
+}
+
+int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) {
+    if (!c || !key || !value) return fail(BPGL_E_ARG, "null argument");
+    if (!strcmp(key, "interleave1")) *value = c->interleave[0];
+    else if (!strcmp(key, "interleave2")) *value = c->interleave[1];
+    else if (!strcmp(key, "d_split")) *value = c->dsplit;
+    else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;
 }
 

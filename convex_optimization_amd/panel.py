@@ -7,10 +7,12 @@ GEMVs, then applies the reference's shrink, exact line search and update to
 every right-hand side (cyclic block order, fixed iteration count).
 
 Numerics (stated tolerance): A is stored as bf16 (the problem is defined by the
-bf16-rounded A); the residual and direction enter the MFMA as hi + lo bf16
-pairs with fp32 accumulation per block tile and fp64 after that.  Against the
-fp64 oracle on the same bf16 A the iterate agrees to <= 1e-2 relative l2 and
-the objective to <= 1e-5 relative (tests/test_panel.py).
+bf16-rounded A); the residual enters the MFMA as a hi + lo bf16 pair, the
+direction as the same pair or (d_split = 1) as its bf16 rounding, with fp32
+accumulation per block tile and fp64 after that.  The line search is exact
+along the direction the MFMA saw.  Against the fp64 oracle on the same bf16 A
+the iterate agrees to <= 1e-2 relative l2 and the objective to <= 1e-5
+relative (tests/test_panel.py), for both d_split settings.
 
 All compute goes through libbpgl.so (bpgl_panel_* in include/bpgl.h).
 """
@@ -41,6 +43,7 @@ _PANEL_SIGS = {
     "bpgl_panel_kernel_times": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "bpgl_panel_geometry": (ctypes.c_int, [_p, ctypes.POINTER(_i32)]),
     "bpgl_panel_set_tuning": (ctypes.c_int, [_p, ctypes.c_char_p, _i64]),
+    "bpgl_panel_get_tuning": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(_i64)]),
 }
 N._SIGS.update(_PANEL_SIGS)
 
@@ -173,8 +176,15 @@ class PanelLasso:
         return self.solver_x_device().to(torch.float64).cpu().numpy().T.copy()   # (n, k)
 
     def set_tuning(self, key, value):
-        """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave' 0-2."""
+        """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave' 0-2.
+        'd_split' 1 / 2: the solver's direction enters the A D pass as its bf16 rounding (1) or as a
+        hi + lo pair (2); both are exact line searches along the direction taken."""
         N.check(_lib().bpgl_panel_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_panel_set_tuning")
+
+    def get_tuning(self, key):
+        v = ctypes.c_int64()
+        N.check(_lib().bpgl_panel_get_tuning(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_panel_get_tuning")
+        return v.value
 
     def set_kernel_timing(self, enable):
         N.check(_lib().bpgl_panel_set_kernel_timing(self._ctx, int(bool(enable))), "bpgl_panel_set_kernel_timing")

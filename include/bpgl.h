@@ -226,9 +226,9 @@ int bpgl_geometry(const bpgl_ctx* ctx, int32_t* nseg, int32_t* nchunk, int32_t* 
 
 /* ===========================================================================
  * Panel path (BASELINE configs[4]): nrhs in {16, 32, 64, 128} right-hand sides
- * solved together, A stored bf16 twice (row-major A [m][lda] and its transpose
- * At [n][ldt], both caller-owned), both passes on CDNA4 MFMA
- * (v_mfma_f32_16x16x32_bf16) with hi+lo bf16 split operands.  The reference
+ * solved together, A stored once in bf16 (row-major A [m][lda], caller-owned;
+ * the A^T pass reads it through transposing LDS reads), both passes on CDNA4
+ * MFMA (v_mfma_f32_16x16x32_bf16) with split-bf16 operands.  The reference
  * has no batched solver: each RHS follows the single-RHS iteration of
  * lasso.py:102-157 (cyclic blocks, fixed iteration count).  m and the block
  * width must be multiples of 256.  Layouts: B, R [nrhs][m]; G, D [nrhs][w];
@@ -253,13 +253,20 @@ const float* bpgl_panel_x(bpgl_panel* ctx);
 int bpgl_panel_set_kernel_timing(bpgl_panel* ctx, int enable);
 int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce (+ line search), step (0: folded into reduce), update */,
                             int64_t* samples);
-/* tuning knobs (results are bitwise independent of them): "interleave1",
+/* tuning knobs.  Results are bitwise independent of these: "interleave1",
  * "interleave2" (pass 1 / pass 2; "interleave" sets both) 0/1/2 -- LDS-DMA
  * pieces issued together after each stage barrier (0), spread over the stage's
  * MFMA groups (1, pass-2 default), or spread and software-pipelined with
  * fragment reads one MFMA group ahead across the stage barrier (2, pass-1
- * default). */
+ * default).
+ * This one selects the solver's arithmetic (every choice is an exact line
+ * search along the direction it takes): "d_split" 2 -- the direction enters
+ * the A D pass as a hi + lo bf16 pair (~16-bit mantissa); 1 -- as its bf16
+ * rounding alone (half the pass-2 MFMA work).  bpgl_panel_mtm / _mm always use
+ * hi + lo operands.  bpgl_panel_get_tuning reads "interleave1", "interleave2",
+ * "d_split". */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
+int bpgl_panel_get_tuning(const bpgl_panel* ctx, const char* key, int64_t* value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
 
 #ifdef __cplusplus

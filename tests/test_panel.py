@@ -63,11 +63,15 @@ def objective(A, b, mu, x):
     return 0.5 * r @ r + mu * np.abs(x).sum()
 
 
+@pytest.mark.parametrize("d_split", [2, 1])
 @pytest.mark.parametrize("m,n,blocks,k,iters", [(512, 2048, 1, 32, 150), (256, 1024, 2, 16, 120),
                                                 (768, 768, 3, 64, 90), (512, 1024, 1, 128, 60)])
-def test_panel_solver_matches_per_rhs_oracle(m, n, blocks, k, iters):
+def test_panel_solver_matches_per_rhs_oracle(m, n, blocks, k, iters, d_split):
+    """Both direction encodings (hi + lo pair, bf16 rounding) meet the stated tolerance."""
     Ab, B, mu = instance(m, n, k, seed=7 + k)
     pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
+    pl.set_tuning("d_split", d_split)
+    assert pl.get_tuning("d_split") == d_split
     res = pl.run(B, mu, iters, record=True)
     assert res["iters"] == iters
     X = res["x"]
@@ -83,9 +87,11 @@ def test_panel_solver_matches_per_rhs_oracle(m, n, blocks, k, iters):
     assert np.all(np.isfinite(res["err_iter"]))
 
 
-def test_panel_graph_equals_eager_and_objective_decreases():
+@pytest.mark.parametrize("d_split", [2, 1])
+def test_panel_graph_equals_eager_and_objective_decreases(d_split):
     Ab, B, mu = instance(256, 1024, 16, seed=3)
     pl = PanelLasso(Ab, 1, nrhs=16, device=0)
+    pl.set_tuning("d_split", d_split)
     a = pl.run(B, mu, 40, use_graph=True)["x"]
     b = pl.run(B, mu, 40, use_graph=False)["x"]
     np.testing.assert_array_equal(a, b)
@@ -99,17 +105,22 @@ def test_panel_graph_equals_eager_and_objective_decreases():
         prev = cur
 
 
-@pytest.mark.parametrize("k", [16, 32, 128])
-def test_panel_interleave_knob_is_bitwise_neutral(k):
+@pytest.mark.parametrize("d_split", [2, 1])
+@pytest.mark.parametrize("k", [16, 32, 64, 128])
+def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
     Ab, B, mu = instance(512, 1024, k, seed=11)
     pl = PanelLasso(Ab, 2, nrhs=k, device=0)
+    pl.set_tuning("d_split", d_split)
     out = []
     for v in (0, 1, 2):
         pl.set_tuning("interleave", v)
         out.append(pl.run(B, mu, 12)["x"])
     np.testing.assert_array_equal(out[0], out[1])
+    np.testing.assert_array_equal(out[0], out[2])
     with pytest.raises(Exception):
         pl.set_tuning("no_such_knob", 1)
+    with pytest.raises(Exception):
+        pl.set_tuning("d_split", 3)
 
 
 @pytest.mark.parametrize("kchunks", [1, 2, 4, 16])
