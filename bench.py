@@ -120,6 +120,14 @@ class Ctx:
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", str(world)))
         self.local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        # rehearsal of the N > 1 code path on a one-GPU box (every rank on this device;
+        # numbers meaningless): BPGL_BENCH_DEVICE=0.  RCCL refuses two ranks of one node on
+        # one GPU, so each rank claims its own host id and the ranks talk over loopback sockets.
+        if os.environ.get("BPGL_BENCH_DEVICE"):
+            self.local = int(os.environ["BPGL_BENCH_DEVICE"])
+            os.environ["NCCL_HOSTID"] = f"bpgl-rehearsal-{self.rank}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
         self.dist = dist
         if self.world > 1:
             dist.init_process_group("gloo")
