@@ -76,7 +76,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=256,
                     help="timed iterations (default 256: with the default warmup the window holds exactly one "
                          "exact-gradient refresh of the one-pass iteration, i.e. its amortised cost)")
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=200,
+                    help="untimed iterations before the window (default 200: the first ~100 ms of steady load "
+                         "run 1-7 %% slower on a fresh box -- measured configs[1] 2912 -> 2939 it/s, configs[4] "
+                         "1849 -> 1976 it/s going from 20/10 to 300/100 warmup iterations)")
     ap.add_argument("--m", type=int, default=M)
     ap.add_argument("--n-per-gpu", type=int, default=N_PER_GPU)
     ap.add_argument("--block", type=int, default=1)
@@ -104,10 +107,16 @@ def parse():
     ap.add_argument("--d-split", type=int, default=-1, choices=[-1, 1, 2],
                     help="panel path: the direction enters the A D pass as a hi + lo bf16 pair (2) or as its "
                          "bf16 rounding (1); -1: library default")
+    ap.add_argument("--write-through", type=int, default=-1,
+                    help="panel path: write-through store sites mask (1 pass-1 epilogue, 2 pass-2 slab, 4 S, "
+                         "8 R; -1: library default)")
+    ap.add_argument("--defer-x", type=int, default=-1, choices=[-1, 0, 1],
+                    help="panel path, one block: apply x += gamma D in the next pass-1 epilogue (1) or in the "
+                         "update kernel (0); -1: library default")
     a = ap.parse_args()
     if a.config == 3:
         a.m, a.n_per_gpu = 1048576, 4096
-        a.steps, a.warmup = min(a.steps, 30), min(a.warmup, 5)
+        a.steps, a.warmup = min(a.steps, 30), min(a.warmup, 40)   # 2.7 ms per iteration
     elif a.config == 4:
         a.rhs = 128
     return a
@@ -324,6 +333,10 @@ def main_panel(args):
         pl.set_tuning("interleave", args.interleave)
     if args.d_split > 0:
         pl.set_tuning("d_split", args.d_split)
+    if args.defer_x >= 0:
+        pl.set_tuning("defer_x", args.defer_x)
+    if args.write_through >= 0:
+        pl.set_tuning("write_through", args.write_through)
     d_split = pl.get_tuning("d_split")
     del A
     Ab = pl.A_bf16.float()
@@ -371,7 +384,8 @@ def main_panel(args):
         "config": {
             "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
-            "interleave": args.interleave, "d_split": d_split,
+            "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
+            "defer_x": pl.get_tuning("defer_x"),
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
             "iter_roofline_frac": iters_s * alg_iter / (HBM_PEAK_GBS * 1e9),

@@ -64,7 +64,8 @@ struct PanelState {
     long long iters;
     double last_err;
     long long cur_mb;   // block of the iteration being finished (set by the line search)
-    long long pad[4];
+    long long pending;  // one feature block: x += gamma D' of the last iteration not yet applied
+    long long pad[3];
 };
 
 struct PanelParams {
@@ -94,6 +95,7 @@ struct PanelParams {
     long long rec_len;
     PanelState* st;
     unsigned long long* cnt;   // [k] k_panel_reduce arrivals per RHS (monotone: launch q ends at q * groups)
+    int wt;             // write-through store sites: 1 pass-1 epilogue (x, D'), 2 pass-2 slab, 4 S, 8 R
 };
 
 constexpr int kLspRows = 1024;    // rows per line-search partial
@@ -414,6 +416,43 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
+// Write-through (sc1) stores for the bulk outputs a kernel hands to the next launch (split-K
+// slab, D', x, S, R and its split): the lines do not sit dirty in the XCD L2s at the kernel
+// boundary, whose cost grows by ~1 us per 6 MB left dirty (MI355X_MICROARCH.md, "boundary").
+// The resource is uniform (a buffer's base); the per-lane part is a byte offset (< 2^31).
+typedef unsigned int pu32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int pu32x2 __attribute__((ext_vector_type(2)));
+constexpr int kPanelSC1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+template <typename V>
+__device__ __forceinline__ void wt_store16(__amdgpu_buffer_rsrc_t r, long long byte_off, const V& v) {
+    static_assert(sizeof(V) == 16, "16-byte store");
+    pu32x4 u;
+    __builtin_memcpy(&u, &v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)byte_off, 0, kPanelSC1);
+}
+template <typename V>
+__device__ __forceinline__ void wt_store8(__amdgpu_buffer_rsrc_t r, long long byte_off, const V& v) {
+    static_assert(sizeof(V) == 8, "8-byte store");
+    pu32x2 u;
+    __builtin_memcpy(&u, &v, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)byte_off, 0, kPanelSC1);
+}
+// element e of a buffer of `count` elements: write-through when `on` (PanelParams::wt, the
+// "write_through" knob) and the buffer's bytes fit a buffer offset (wave-uniform tests), a
+// plain store otherwise
+template <typename V, typename E>
+__device__ __forceinline__ void wt_put(bool on, E* base, long long count, long long e, const V& v) {
+    if (on && count * (long long)sizeof(E) < (1ll << 31)) {
+        if constexpr (sizeof(V) == 16) wt_store16(wt_rsrc(base), e * (long long)sizeof(E), v);
+        else wt_store8(wt_rsrc(base), e * (long long)sizeof(E), v);
+    } else {
+        *reinterpret_cast<V*>(base + e) = v;
+    }
+}
+
 __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
     const float f = (float)v;
     hi = to_bf16(f);
@@ -457,17 +496,36 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
         return;
     }
     double* nred = reinterpret_cast<double*>(smem);   // [4 wm][k][3]
+    // one feature block: the previous iteration's x += gamma D' (k_panel_update leaves it
+    // pending) is applied here, from the D' this thread is about to overwrite -- the same
+    // arithmetic as k_panel_update's x part, so x is bitwise unchanged by the deferral
+    const bool fx = p.st->pending != 0;
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int nt = 0; nt < G::NTW; ++nt) {
         const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
         const double mu = p.mu[rhs];
+        const double gprev = fx ? p.gamma[rhs] : 0.0;
         double sbx = 0.0, sx = 0.0, err = 0.0;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
             const long long j = c0 + wm * 64 + mt * 16 + (lane >> 4) * 4;   // 4 consecutive columns
-            const float* xp = p.X + ((long long)mb * p.k + rhs) * p.w + j;
+            float* xp = p.X + ((long long)mb * p.k + rhs) * p.w + j;
             const float4 x4 = *reinterpret_cast<const float4*>(xp);
-            const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+            float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+            if (fx) {
+                const bf16x4 ph = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.w + j);
+                bf16x4 pl;
+                if constexpr (DS == 2) pl = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.w + j);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    double dq = (double)(float)ph[r];
+                    if constexpr (DS == 2) dq += (double)(float)pl[r];
+                    xs[r] = (float)((double)xs[r] + gprev * dq);
+                }
+                wt_put(p.wt & 1, p.X, (long long)p.nblock * p.k * p.w, ((long long)mb * p.k + rhs) * p.w + j,
+                       make_float4(xs[0], xs[1], xs[2], xs[3]));
+            }
             __bf16 dh[4], dl[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -488,10 +546,9 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
                 const double e = fabs(g - proj(g - x, -mu, mu));
                 err = (e > err || e != e) ? e : err;
             }
-            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<bf16x4*>(p.Dh + (long long)rhs * p.w + j) = bf16x4{dh[0], dh[1], dh[2], dh[3]};
+            wt_put(p.wt & 1, p.Dh, (long long)p.k * p.w, (long long)rhs * p.w + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
             if constexpr (DS == 2)
-                *reinterpret_cast<bf16x4*>(p.Dl + (long long)rhs * p.w + j) = bf16x4{dl[0], dl[1], dl[2], dl[3]};
+                wt_put(p.wt & 1, p.Dl, (long long)p.k * p.w, (long long)rhs * p.w + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
         }
         // lanes l, l^16, l^32, l^48 share the RHS
         sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
@@ -559,9 +616,8 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, 
         for (int nt = 0; nt < G::NTW; ++nt) {
             const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
             const long long row = r0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
-            float* dst = p.Sslab + ((long long)chunk * p.k + rhs) * p.m + row;
-            *reinterpret_cast<float4*>(dst) = make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2],
-                                                          acc[mt][nt][3]);
+            wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
+                   make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
         }
 }
 
@@ -593,9 +649,9 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
             s[2] += (double)v.z;
             s[3] += (double)v.w;
         }
-        double* so = Sout + (long long)rhs * p.m + i;
-        *reinterpret_cast<double2*>(so) = make_double2(s[0], s[1]);
-        *reinterpret_cast<double2*>(so + 2) = make_double2(s[2], s[3]);
+        const long long e = (long long)rhs * p.m + i;
+        wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e, make_double2(s[0], s[1]));
+        wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e + 2, make_double2(s[2], s[3]));
         if (mode) {
             const double* r = p.R + (long long)rhs * p.m + i;
             const double2 r01 = *reinterpret_cast<const double2*>(r);
@@ -647,23 +703,53 @@ __device__ void panel_step_rhs(const PanelParams& p, int rhs) {
     b = wave_sum(b);
     e = wave_max(e);
     if (lane == 0) { s3[0][wave] = a; s3[1][wave] = b; s3[2][wave] = e; }
-    __syncthreads();
+    // the line-search partials of the 1024-row groups: loaded in parallel (one group per
+    // thread), summed by thread 0 in group order -- a serial chain of dependent loads cost ~1 us
+    // per group
+    __shared__ double lsr[kThreads][2];
+    double rs = 0.0, ss = 0.0;
+    const int ng = (int)((p.m + kLspRows - 1) / kLspRows);
+    for (int g0 = 0; g0 < ng; g0 += kThreads) {
+        const int g = g0 + (int)threadIdx.x;
+        if (g < ng) {
+            const double* q = p.lsp + ((long long)g * p.k + rhs) * 2;
+            lsr[threadIdx.x][0] = LSP_SC1 ? panel_ld_sc1(q) : q[0];
+            lsr[threadIdx.x][1] = LSP_SC1 ? panel_ld_sc1(q + 1) : q[1];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < kThreads && g0 + i < ng; ++i) { rs += lsr[i][0]; ss += lsr[i][1]; }
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
         a = ((s3[0][0] + s3[0][1]) + s3[0][2]) + s3[0][3];
         b = ((s3[1][0] + s3[1][1]) + s3[1][2]) + s3[1][3];
         e = s3[2][0];
         for (int q = 1; q < kWaves; ++q) e = (s3[2][q] > e || s3[2][q] != s3[2][q]) ? s3[2][q] : e;
-        double rs = 0.0, ss = 0.0;
-        const int ng = (int)((p.m + kLspRows - 1) / kLspRows);
-        for (int g = 0; g < ng; ++g) {
-            const double* q = p.lsp + ((long long)g * p.k + rhs) * 2;
-            rs += LSP_SC1 ? panel_ld_sc1(q) : q[0];
-            ss += LSP_SC1 ? panel_ld_sc1(q + 1) : q[1];
-        }
         const double r1 = rs + p.mu[rhs] * (a - b);
         p.gamma[rhs] = (ss == 0.0) ? 0.0 : proj(-r1 / ss, 0.0, 1.0);
         p.err_rhs[rhs] = e;
         if (rhs == 0) p.st->cur_mb = p.st->t % p.nblock;   // nobody else reads it in this launch
+    }
+}
+
+// end of an iteration (wave 0 of block 0 of the update launch): the max error over the RHS
+// (one load per lane, then the wave max -- a serial loop over k dependent loads cost ~10 us),
+// the error record, t + 1; `pending`: x += gamma D' is left to the next pass-1 epilogue
+__device__ __forceinline__ void panel_bump_t(const PanelParams& p, bool pending) {
+    double e = 0.0;
+    for (int j = threadIdx.x; j < p.k; j += 64) {
+        const double v = p.err_rhs[j];
+        e = (v > e || v != v) ? v : e;
+    }
+    e = wave_max(e);
+    if (threadIdx.x == 0) {
+        const long long t = p.st->t;
+        if (p.err_iter && t < p.rec_len) p.err_iter[t] = e;
+        p.st->last_err = e;
+        p.st->t = t + 1;
+        p.st->iters = t + 1;
+        if (pending) p.st->pending = 1;
     }
 }
 
@@ -721,21 +807,71 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
                 r[q] = acc[q] - p.B[e + q];
                 split_bf16(r[q], hi[q], lo[q]);
             }
-            *reinterpret_cast<double2*>(p.R + e) = make_double2(r[0], r[1]);
-            *reinterpret_cast<double2*>(p.R + e + 2) = make_double2(r[2], r[3]);
-            *reinterpret_cast<bf16x4v*>(p.Rh + e) = bf16x4v{hi[0], hi[1], hi[2], hi[3]};
-            *reinterpret_cast<bf16x4v*>(p.Rl + e) = bf16x4v{lo[0], lo[1], lo[2], lo[3]};
+            wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
+            wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
+            wt_put(p.wt & 8, p.Rh, nr, e, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+            wt_put(p.wt & 8, p.Rl, nr, e, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const long long t = p.st->t;
-        double emax = 0.0;
-        for (int j = 0; j < p.k; ++j) emax = (p.err_rhs[j] > emax || p.err_rhs[j] != p.err_rhs[j]) ? p.err_rhs[j] : emax;
-        if (p.err_iter && t < p.rec_len) p.err_iter[t] = emax;
-        p.st->last_err = emax;
-        p.st->t = t + 1;
-        p.st->iters = t + 1;
+    if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, false);
+}
+
+// One feature block: R_j += gamma_j S_j (= Ax_j + gamma_j S_j - B_j; Ax is not kept) and its
+// hi/lo split; x += gamma D' is left pending for the next pass-1 epilogue (or k_panel_flush).
+// A thread owns 4 consecutive residual rows.  Also bumps t.
+__global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p) {
+    const long long nr = (long long)p.k * p.m;
+    const unsigned ur = (unsigned)(nr / 4), m4 = (unsigned)(p.m / 4);
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+    for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
+        const long long e = 4ll * v;
+        const double g = p.gamma[v / m4];
+        const double2 r01 = *reinterpret_cast<const double2*>(p.R + e);
+        const double2 r23 = *reinterpret_cast<const double2*>(p.R + e + 2);
+        const double2 s01 = *reinterpret_cast<const double2*>(p.S + e);
+        const double2 s23 = *reinterpret_cast<const double2*>(p.S + e + 2);
+        const double r[4] = {r01.x + g * s01.x, r01.y + g * s01.y, r23.x + g * s23.x, r23.y + g * s23.y};
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split_bf16(r[q], hi[q], lo[q]);
+        wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
+        wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
+        wt_put(p.wt & 8, p.Rh, nr, e, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+        wt_put(p.wt & 8, p.Rl, nr, e, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
     }
+    if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, true);
+}
+
+// apply a pending x += gamma D' (one feature block) -- the end of every bpgl_panel_step, so the
+// iterates the caller reads are current; a no-op when nothing is pending
+template <int DS>
+__global__ __launch_bounds__(kThreads) void k_panel_flush(PanelParams p) {
+    if (p.st->pending == 0) return;
+    const long long nx = (long long)p.k * p.w;
+    typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+    const unsigned w8 = (unsigned)(p.w / 8);
+    for (unsigned u = blockIdx.x * kThreads + threadIdx.x; u < (unsigned)(nx / 8); u += gridDim.x * kThreads) {
+        const long long e = 8ll * u;
+        const double g = p.gamma[u / w8];
+        const bf16x8v dh = *reinterpret_cast<const bf16x8v*>(p.Dh + e);
+        bf16x8v dl;
+        if constexpr (DS == 2) dl = *reinterpret_cast<const bf16x8v*>(p.Dl + e);
+        float* xp = p.X + e;
+        float4 x0 = *reinterpret_cast<const float4*>(xp);
+        float4 x1 = *reinterpret_cast<const float4*>(xp + 4);
+        float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            double dq = (double)(float)dh[q];
+            if constexpr (DS == 2) dq += (double)(float)dl[q];
+            xs[q] = (float)((double)xs[q] + g * dq);
+        }
+        *reinterpret_cast<float4*>(xp) = make_float4(xs[0], xs[1], xs[2], xs[3]);
+        *reinterpret_cast<float4*>(xp + 4) = make_float4(xs[4], xs[5], xs[6], xs[7]);
+    }
+}
+__global__ void k_panel_clear_pending(PanelParams p) {
+    if (threadIdx.x == 0) p.st->pending = 0;
 }
 
 // split an fp64 [k][len] operand into hi/lo bf16; optionally R = -B (reset)
@@ -782,6 +918,7 @@ __global__ void k_panel_reset_state(PanelParams p) {
         p.st->iters = 0;
         p.st->last_err = 0.0;
         p.st->cur_mb = 0;
+        p.st->pending = 0;
     }
 }
 

@@ -34,6 +34,8 @@ struct bpgl_panel {
     bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
     int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
     int dsplit = 2;               // bf16 pieces of the solver's direction (d_split knob)
+    int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
+    int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
 };
 
 namespace {
@@ -138,10 +140,15 @@ int panel_iteration(bpgl_panel* c, int64_t it) {
     if ((rc = panel_reduce(c, c->p.S, 1))) return rc;   // its last block per RHS runs the line search
     panel_ev(c, it, 2, 1);
     panel_ev(c, it, 4, 0);
-    const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
-    const dim3 ug((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192));
-    if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_update<1>, ug, dim3(kThreads), 0, c->stream, c->p);
-    else hipLaunchKernelGGL(k_panel_update<2>, ug, dim3(kThreads), 0, c->stream, c->p);
+    if (c->nblock == 1 && c->defer_x) {   // R only; x += gamma D' rides on the next pass-1 epilogue (or the flush)
+        const dim3 ug((unsigned)std::min<int64_t>(cdiv((int64_t)c->k * c->m / 4, kThreads), 8192));
+        hipLaunchKernelGGL(k_panel_update1, ug, dim3(kThreads), 0, c->stream, c->p);
+    } else {
+        const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
+        const dim3 ug((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192));
+        if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_update<1>, ug, dim3(kThreads), 0, c->stream, c->p);
+        else hipLaunchKernelGGL(k_panel_update<2>, ug, dim3(kThreads), 0, c->stream, c->p);
+    }
     LAUNCH_CHECK("k_panel_update");
     panel_ev(c, it, 4, 1);
     return 0;
@@ -251,6 +258,7 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.gamma = (double*)(s + L.gamma);
     p.err_rhs = (double*)(s + L.err_rhs);
     p.cnt = (unsigned long long*)(s + L.cnt);
+    p.wt = c->wt;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
     c->bound = true;
@@ -347,6 +355,14 @@ int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
         if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
         if (c->timing) c->timed_iters++;
     }
+    if (c->nblock == 1 && c->defer_x) {   // the last iteration's x update, so X is current between calls
+        const dim3 fg((unsigned)std::min<int64_t>(cdiv((int64_t)c->k * c->w / 8, kThreads), 8192));
+        if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_flush<1>, fg, dim3(kThreads), 0, c->stream, c->p);
+        else hipLaunchKernelGGL(k_panel_flush<2>, fg, dim3(kThreads), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_panel_flush");
+        hipLaunchKernelGGL(k_panel_clear_pending, dim3(1), dim3(64), 0, c->stream, c->p);
+        LAUNCH_CHECK("k_panel_clear_pending");
+    }
     return 0;
 }
 
@@ -398,6 +414,14 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
         if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
+    } else if (!strcmp(key, "write_through")) {
+        if (value < 0 || value > 15) return fail(BPGL_E_ARG, "write_through is a mask of 4 bits");
+        c->wt = (int)value;
+        c->p.wt = c->wt;
+    } else if (!strcmp(key, "defer_x")) {
+        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "defer_x must be 0 or 1");
+        c->defer_x = (int)value;
+        c->solver = false;   // the two forms keep different state (Ax): a reset must follow
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;
@@ -413,6 +437,8 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     if (!strcmp(key, "interleave1")) *value = c->interleave[0];
     else if (!strcmp(key, "interleave2")) *value = c->interleave[1];
     else if (!strcmp(key, "d_split")) *value = c->dsplit;
+    else if (!strcmp(key, "write_through")) *value = c->wt;
+    else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;
 }

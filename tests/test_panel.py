@@ -165,3 +165,28 @@ def test_panel_rejects_bad_shapes():
         PanelLasso(np.ones((256, 256)), 1, nrhs=24)
     with pytest.raises(Exception):
         PanelLasso(np.ones((256, 384)), 1, nrhs=16)
+
+
+@pytest.mark.parametrize("d_split", [2, 1])
+def test_panel_deferred_x_update_agrees(d_split):
+    """One block: x += gamma D' applied in the next pass-1 epilogue (defer_x 1, R updated
+    incrementally) vs in the update kernel (defer_x 0, R = Ax - B): the same iterates up to
+    the fp64 rounding of R (split-K-like tolerance); x is current after every step call."""
+    Ab, B, mu = instance(512, 1024, 32, seed=13)
+    out = {}
+    for dx in (0, 1):
+        pl = PanelLasso(Ab, 1, nrhs=32, device=0)
+        pl.set_tuning("d_split", d_split)
+        pl.set_tuning("defer_x", dx)
+        assert pl.get_tuning("defer_x") == dx
+        pl.solver_reset(B, mu)
+        xs = []
+        for _ in range(3):
+            pl.solver_step(7)
+            xs.append(pl.solver_x())
+        out[dx] = xs
+    for a, b in zip(out[0], out[1]):
+        assert np.linalg.norm(a - b) <= 1e-4 * np.linalg.norm(a)
+    pl.set_tuning("defer_x", 0)
+    with pytest.raises(Exception):
+        pl.solver_step(1)   # the two forms keep different state: a change needs a reset
