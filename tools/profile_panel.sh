@@ -12,7 +12,7 @@ cd /tmp
 B="python3 $R/bench.py --rhs $K --steps 6 --warmup 2 --no-cpu"
 RX="k_panel_pass"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -- \
-    python3 $R/bench.py --rhs $K --steps 50 --warmup 10 --no-cpu > $OUT/bench_trace.json 2> $OUT/trace.err
+    python3 $R/bench.py --rhs $K --steps 100 --warmup 100 --no-cpu > $OUT/bench_trace.json 2> $OUT/trace.err
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
     SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $OUT/sq \
     --kernel-include-regex "$RX" -- $B > $OUT/b_sq.json 2> $OUT/sq.err

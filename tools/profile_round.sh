@@ -11,9 +11,9 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -- \
-    python3 $R/bench.py --steps 50 --warmup 10 --no-cpu > $OUT/bench_trace.json 2> $OUT/trace.err
+    python3 $R/bench.py --steps 256 --warmup 100 --no-cpu > $OUT/bench_trace.json 2> $OUT/trace.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_c3 -- \
-    python3 $R/bench.py --config 3 --steps 20 --warmup 4 --no-cpu > $OUT/bench_trace_c3.json 2> $OUT/trace_c3.err
+    python3 $R/bench.py --config 3 --steps 30 --warmup 40 --no-cpu > $OUT/bench_trace_c3.json 2> $OUT/trace_c3.err
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch \
     --kernel-include-regex "k_iter_a|k_iter_b|k_colpass|k_rowpass|k_onepass" -- \
     python3 $R/bench.py --steps 6 --warmup 2 --no-cpu > $OUT/bench_fetch.json 2> $OUT/fetch.err
