@@ -419,6 +419,19 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
     for (long long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {   // block-uniform
         const long long j = tile * 64 + lane;
         const bool ok = j < p.wp;
+        const bool col = ok && j < p.w;
+        // wave 0's column operands are loaded before the U fold and its barrier, so both sets of
+        // loads are in flight together (one memory round trip instead of two)
+        double g = 0.0, xj = 0.0, dold = 0.0, dg = 0.0, rc = 0.0;
+        if (wave == 0 && ok) {
+            g = o.G[j];
+            if (col) {
+                xj = p.x[j];
+                if (UPDATE) dold = p.D[j];
+                dg = p.diag[j];
+                rc = p.rec[j];
+            }
+        }
         if (UPDATE) {
             double acc = 0.0;
             if (ok) {
@@ -429,21 +442,19 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
             __syncthreads();
         }
         if (wave == 0 && ok) {
-            double g = o.G[j];
             if (UPDATE) {
                 g += gamma * (((ured[0][lane] + ured[1][lane]) + ured[2][lane]) + ured[3][lane]);
                 o.G[j] = g;
             }
             p.g[j] = g;
             double Dj = 0.0;
-            if (j < p.w) {
-                double xj = p.x[j];
+            if (col) {
                 if (UPDATE) {
-                    xj += gamma * p.D[j];
+                    xj += gamma * dold;
                     p.x[j] = xj;
                 }
-                const double rx = p.diag[j] * xj - g;                 // lasso.py:114
-                const double bx = p.rec[j] * soft_thr(rx, p.mu);      // lasso.py:115-117
+                const double rx = dg * xj - g;                        // lasso.py:114
+                const double bx = rc * soft_thr(rx, p.mu);            // lasso.py:115-117
                 Dj = bx - xj;                                         // lasso.py:119
                 abx += fabs(bx);
                 ax1 += fabs(xj);
