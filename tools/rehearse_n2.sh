@@ -5,6 +5,6 @@
 # JSON line) works end to end.  Usage (GPU box): tools/rehearse_n2.sh [extra bench args]
 set -o pipefail
 mkdir -p gpurun_out/rehearse
-BPGL_BENCH_DEVICE=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 16 --warmup 4 --no-cpu "$@" \
-    > gpurun_out/rehearse/bench_n2.json 2> gpurun_out/rehearse/bench_n2.err
+BPGL_BENCH_DEVICE=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NPROC:-2} \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus ${NPROC:-2} --steps 16 --warmup 4 --no-cpu "$@" \
+    > gpurun_out/rehearse/bench_n${NPROC:-2}.json 2> gpurun_out/rehearse/bench_n${NPROC:-2}.err
