@@ -435,7 +435,9 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
         if (UPDATE) {
             double acc = 0.0;
             if (ok) {
-#pragma unroll 4
+                // 16 loads in flight per lane (configs[3]: 256 row groups, 64 per wave); the adds stay
+                // in group order
+#pragma unroll 16
                 for (int q = wave; q < o.ngroups; q += kWaves) acc += o.Us[(long long)q * p.wp + j];
             }
             ured[wave][lane] = acc;
