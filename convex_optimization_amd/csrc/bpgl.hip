@@ -96,6 +96,7 @@ struct bpgl_ctx {
     // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
     // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
     bool rows = false;
+    int xch32 = 1;   // RCCL row shards: the per-iteration all-reduce in fp32 ("exchange_fp32")
     bool op_refresh_pending = false;   // external rows: phase 2 ran, phase 3 not yet
     int64_t op_t = 0;          // iterations enqueued since the solver reset
     OnePassArgs op{};
@@ -257,7 +258,8 @@ int rowreduce_p(bpgl_ctx* c, const Params& q, const double* slab, double* out, i
     else hipLaunchKernelGGL(k_rowreduce<16>, g, b, 0, c->stream, q, slab, out, mode);
     LAUNCH_CHECK("k_rowreduce");
     if (mode == 1) {
-        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, q, (int)rowreduce_blocks(c));
+        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, q, (int)rowreduce_blocks(c),
+                           (const float*)nullptr);
         LAUNCH_CHECK("k_linesearch");
     }
     return 0;
@@ -343,11 +345,16 @@ int onepass_launch(bpgl_ctx* c) {
 }
 // the one-pass tail's view of U: the row-group partials (one rank), or the all-reduced sum
 // in the exchange buffer (row shards)
+// RCCL row shards exchange [U | r.s23 | s23.s23] in fp32 (U rounded, the scalars as hi + lo
+// pairs): half the all-reduce bytes; measured drift DESIGN.md section 6.  The caller-side
+// (external) exchange and the exact-gradient refresh stay fp64.
+bool xch_f32(const bpgl_ctx* c) { return c->rows && c->comm && !c->external && c->xch32; }
 OnePassArgs op_tail_args(const bpgl_ctx* c) {
     OnePassArgs o = c->op;
     if (c->rows) {
         o.Us = c->p.comm;
         o.ngroups = 1;
+        if (xch_f32(c)) o.Uf = reinterpret_cast<const float*>(c->p.comm);
     }
     return o;
 }
@@ -473,19 +480,26 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
         if ((rc = onepass_launch(c))) return rc;
         ev_record(c, it, 7, 1);
         ev_record(c, it, 3, 0);
+        float* xf = xch_f32(c) ? reinterpret_cast<float*>(c->p.comm) : nullptr;
         hipLaunchKernelGGL(k_onepass_fold, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024)),
-                           dim3(kThreads), 0, c->stream, c->p, c->op, c->p.comm);
+                           dim3(kThreads), 0, c->stream, c->p, c->op, c->p.comm, xf);
         LAUNCH_CHECK("k_onepass_fold");
         ev_record(c, it, 3, 1);
         if (c->comm) {
             ev_record(c, it, 4, 0);
-            if ((rc = allreduce_sum(c, c->p.comm, c->wp + 2))) return rc;
+            if (xf) {
+                ncclResult_t nr = ncclAllReduce(xf, xf, (size_t)(c->wp + 4), ncclFloat32, ncclSum, c->comm, c->stream);
+                if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
+            } else if ((rc = allreduce_sum(c, c->p.comm, c->wp + 2))) {
+                return rc;
+            }
             ev_record(c, it, 4, 1);
         }
     }
     if ((phase == 0 && !c->external) || (phase == 1 && c->external)) {
         ev_record(c, it, 5, 0);
-        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, ls, 1);
+        const float* pf = xch_f32(c) ? reinterpret_cast<const float*>(c->p.comm) + c->wp : nullptr;
+        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, ls, 1, pf);
         LAUNCH_CHECK("k_linesearch");
         ev_record(c, it, 5, 1);
     }
@@ -1049,6 +1063,12 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         if (value < 0 || value > 1000) return fail(BPGL_E_ARG, "onepass_cache_permille must be in [0, 1000]");
         c->op_cache = (int)value;
         c->op.cache_permille = c->op_cache;
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "exchange_fp32")) {
+        c->xch32 = value != 0;
         drop_graphs(c);
         c->solver = false;
         return 0;

@@ -646,10 +646,16 @@ __global__ __launch_bounds__(kThreads) void k_rowreduce(Params p, const double* 
 // linesearch (one rank): fold the rowreduce and shrink partials in a fixed
 // order and run the line search + stopping rule.  One block.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void k_linesearch(Params p, int nblocks_rr) {
+// `pf` (row shards, fp32 exchange): the summed scalars as hi + lo fp32 pairs [rs_hi, rs_lo,
+// ss_hi, ss_lo] instead of the fp64 parts2 partials.
+__global__ __launch_bounds__(kThreads) void k_linesearch(Params p, int nblocks_rr, const float* __restrict__ pf) {
     if (p.st->done) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double rs = 0.0, ss = 0.0;
+    if (pf) {
+        if (threadIdx.x == 0) { rs = (double)pf[0] + (double)pf[1]; ss = (double)pf[2] + (double)pf[3]; }
+        nblocks_rr = 0;
+    }
 #pragma unroll 8
     for (int k = threadIdx.x; k < nblocks_rr; k += kThreads) {
         rs += p.parts2[2ll * k];

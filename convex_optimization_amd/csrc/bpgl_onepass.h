@@ -56,6 +56,7 @@ struct OnePassArgs {
     int SB, ngroups, R, xl;      // segment blocks per row, row groups, rows per group, XCD-local map
     int ls;                      // 1: the last row group to finish runs the line search (one rank)
     int cache_permille;          // share of each group's rows read last with cache-allocating loads
+    const float* Uf;             // row shards, fp32 exchange: the all-reduced U (read instead of Us)
 };
 
 typedef unsigned long long op_u64;
@@ -363,19 +364,33 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
 
 // Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23]
 // (fixed order over the row groups).  Runs whether or not the solver stopped: the all-reduce
-// after it runs in every iteration of a captured graph.
-__global__ __launch_bounds__(kThreads) void k_onepass_fold(Params p, OnePassArgs o, double* __restrict__ out) {
+// after it runs in every iteration of a captured graph.  `outf` (RCCL row shards, the
+// "exchange_fp32" knob): the same contribution as fp32 -- U rounded, each scalar as a hi + lo
+// pair [U (wp) | rs_hi | rs_lo | ss_hi | ss_lo] -- half the bytes on xGMI.
+__device__ __forceinline__ void op_split_f32(double v, float* dst) {
+    const float hi = (float)v;
+    dst[0] = hi;
+    dst[1] = (float)(v - (double)hi);
+}
+__global__ __launch_bounds__(kThreads) void k_onepass_fold(Params p, OnePassArgs o, double* __restrict__ out,
+                                                           float* __restrict__ outf) {
     const long long stride = (long long)gridDim.x * kThreads;
     for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < p.wp; j += stride) {
         double acc = 0.0;
         for (int q = 0; q < o.ngroups; ++q) acc += o.Us[(long long)q * p.wp + j];
-        out[j] = acc;
+        if (outf) outf[j] = (float)acc;
+        else out[j] = acc;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         double rs = 0.0, ss = 0.0;
         for (int q = 0; q < o.ngroups; ++q) { rs += p.parts2[2ll * q]; ss += p.parts2[2ll * q + 1]; }
-        out[p.wp] = rs;
-        out[p.wp + 1] = ss;
+        if (outf) {
+            op_split_f32(rs, outf + p.wp);
+            op_split_f32(ss, outf + p.wp + 2);
+        } else {
+            out[p.wp] = rs;
+            out[p.wp + 1] = ss;
+        }
     }
 }
 
@@ -438,7 +453,8 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
                 // 16 loads in flight per lane (configs[3]: 256 row groups, 64 per wave); the adds stay
                 // in group order
 #pragma unroll 16
-                for (int q = wave; q < o.ngroups; q += kWaves) acc += o.Us[(long long)q * p.wp + j];
+                for (int q = wave; q < o.ngroups; q += kWaves)
+                    acc += o.Uf ? (double)o.Uf[j] : o.Us[(long long)q * p.wp + j];   // Uf: ngroups = 1
             }
             ured[wave][lane] = acc;
             __syncthreads();

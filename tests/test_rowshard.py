@@ -120,11 +120,35 @@ def test_single_rank_rccl_rows_matches_onepass():
     plain = make_cls("float")(A, 1, device=0).run(b, mu, 150)
     rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
     np.testing.assert_allclose(rows.diag_ATA, make_cls("float")(A, 1, device=0).diag_ATA, rtol=1e-15)
+    rows.set_tuning("exchange_fp32", 0)            # the fp64 exchange: the same sums as one rank
     g1 = rows.run(b, mu, 150, use_graph=True)
     g0 = rows.run(b, mu, 150, use_graph=False)
     np.testing.assert_array_equal(g1["x"], g0["x"])
     assert g1["iters"] == 150
     assert rel(g1["x"], plain["x"]) <= 1e-10, rel(g1["x"], plain["x"])
+
+
+def test_single_rank_rccl_rows_fp32_exchange():
+    """the default RCCL row exchange in fp32 (U rounded, the line-search scalars as hi + lo
+    pairs): graph = eager bitwise, within 1e-6 of the fp64 exchange and within the north_star
+    1e-5 of the oracle (measured 1.8e-7 after 300 iterations, the size of the trajectory's
+    rounding-order sensitivity)"""
+    rs = np.random.RandomState(8)
+    m, n = 1500, 12000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    f1 = rows.run(b, mu, 300, use_graph=True)
+    f0 = rows.run(b, mu, 300, use_graph=False)
+    np.testing.assert_array_equal(f1["x"], f0["x"])
+    rows.set_tuning("exchange_fp32", 0)
+    d = rows.run(b, mu, 300)
+    A32 = A.astype(np.float32).astype(np.float64)
+    orc = oracle.run(A32, b, mu, 1, 300)["x"]
+    print(f"fp32 exchange: vs fp64 exchange {rel(f1['x'], d['x']):.2e}, vs oracle {rel(f1['x'], orc):.2e}")
+    assert rel(f1["x"], d["x"]) <= 1e-6, rel(f1["x"], d["x"])
+    assert rel(f1["x"], orc) <= 1e-5, rel(f1["x"], orc)
 
 
 def test_two_granules_per_lane_width():
@@ -138,6 +162,7 @@ def test_two_granules_per_lane_width():
     two = gc.run(b, mu, 10)
     assert rel(one["x"], two["x"]) <= 1e-10, rel(one["x"], two["x"])
     rows = make_cls("float")(gc._A_dev, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    rows.set_tuning("exchange_fp32", 0)
     r = rows.run(b, mu, 10)
     assert rel(r["x"], one["x"]) <= 1e-12, rel(r["x"], one["x"])
 
@@ -190,6 +215,7 @@ def test_two_granules_ragged_width_with_records():
     plain.set_tuning("onepass", 0)
     two = plain.run(b, mu, 60, err_bound=1e-3, record=True)
     rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    rows.set_tuning("exchange_fp32", 0)
     one = rows.run(b, mu, 60, err_bound=1e-3, record=True)
     assert one["t_last"] == two["t_last"] and one["stopped"] == two["stopped"]
     assert rel(one["x"], two["x"]) <= 1e-10, rel(one["x"], two["x"])

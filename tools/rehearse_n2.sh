@@ -2,9 +2,12 @@
 # Rehearsal of bench.py's N > 1 path on a one-GPU box: two ranks under torch.distributed.run,
 # both on device 0 (BPGL_BENCH_DEVICE=0).  Throughput numbers are meaningless; the run checks
 # that the multi-rank code path (gloo side channel, RCCL communicator, row shards, strong leg,
-# JSON line) works end to end.  Usage (GPU box): tools/rehearse_n2.sh [extra bench args]
+# JSON line) works end to end.  Default split: columns -- the row split's k_onepass needs all of its
+# blocks co-resident, which ranks sharing one GPU cannot guarantee (it then stops with
+# BPGL_E_EXCHANGE by design); `--shard rows` may be passed and passes when the ranks interleave.
+# Usage (GPU box): [NPROC=N] tools/rehearse_n2.sh [extra bench args]
 set -o pipefail
 mkdir -p gpurun_out/rehearse
 BPGL_BENCH_DEVICE=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NPROC:-2} \
-    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus ${NPROC:-2} --steps 16 --warmup 4 --no-cpu "$@" \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus ${NPROC:-2} --steps 16 --warmup 4 --no-cpu --shard columns "$@" \
     > gpurun_out/rehearse/bench_n${NPROC:-2}.json 2> gpurun_out/rehearse/bench_n${NPROC:-2}.err
