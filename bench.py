@@ -99,9 +99,9 @@ def parse():
     ap.add_argument("--shard", default="rows", choices=["rows", "columns"],
                     help="multi-GPU split (N > 1, or N = 1 with --comm): rows (default; one pass over A, "
                          "all-reduce of n + 2) or columns (the reference's split; two passes, all-reduce of m + 2 + N)")
-    ap.add_argument("--exchange-fp32", type=int, default=-1, choices=[-1, 0, 1],
-                    help="RCCL row shards: the per-iteration all-reduce of [U | r.s23 | s23.s23] in fp32 (1, the "
-                         "library default) or fp64 (0)")
+    ap.add_argument("--exchange-fp32", type=int, default=0, choices=[0, 1],
+                    help="RCCL row shards: the per-iteration all-reduce of [U | r.s23 | s23.s23] in fp32 (1, opt-in: "
+                         "half the bytes, x within ~1e-6 of the fp64 exchange) or fp64 (0, default)")
     ap.add_argument("--rhs", type=int, default=1,
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
@@ -196,8 +196,8 @@ def measure(ctx, args, m, n_total):
     gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard)
     gc.set_tuning("fused", args.fused)
     gc.set_tuning("onepass", args.onepass)
-    if args.exchange_fp32 >= 0:
-        gc.set_tuning("exchange_fp32", args.exchange_fp32)
+    if args.exchange_fp32:
+        gc.set_tuning("exchange_fp32", -1)
     gc.set_tuning("onepass_variant", args.onepass_variant)
     if args.onepass_cache >= 0:
         gc.set_tuning("onepass_cache_permille", args.onepass_cache)
@@ -486,7 +486,7 @@ def main():
             "m": m, "n": n_total, "m_local": ml, "n_local": w, "feature_blocks": args.block,
             "a_storage": args.type, "accumulate": "fp64",
             "parallelism": f"{'row' if rows else 'column'}-shard x{G}", "rccl": bool(G > 1 or args.comm),
-            "exchange": ("fp32 (U rounded, scalars hi+lo)" if rows and (G > 1 or args.comm) and args.exchange_fp32 != 0
+            "exchange": ("fp32 (U rounded, scalars hi+lo)" if rows and (G > 1 or args.comm) and args.exchange_fp32
                          else "fp64"),
             "global_iters_per_s": iters_s_graph,
             "iteration": ("one pass over A (k_onepass: s23 = A D and U = A^T s23 together; g += gamma U, "

@@ -96,7 +96,7 @@ struct bpgl_ctx {
     // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
     // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
     bool rows = false;
-    int xch32 = 1;   // RCCL row shards: the per-iteration all-reduce in fp32 ("exchange_fp32")
+    int xch32 = 0;   // row shards' per-iteration exchange in fp32 ("exchange_fp32"; opt-in, -1 = RCCL only)
     bool op_refresh_pending = false;   // external rows: phase 2 ran, phase 3 not yet
     int64_t op_t = 0;          // iterations enqueued since the solver reset
     OnePassArgs op{};
@@ -345,10 +345,14 @@ int onepass_launch(bpgl_ctx* c) {
 }
 // the one-pass tail's view of U: the row-group partials (one rank), or the all-reduced sum
 // in the exchange buffer (row shards)
-// RCCL row shards exchange [U | r.s23 | s23.s23] in fp32 (U rounded, the scalars as hi + lo
-// pairs): half the all-reduce bytes; measured drift DESIGN.md section 6.  The caller-side
-// (external) exchange and the exact-gradient refresh stay fp64.
-bool xch_f32(const bpgl_ctx* c) { return c->rows && c->comm && !c->external && c->xch32; }
+// Row shards exchange [U | r.s23 | s23.s23] in fp32 (U rounded, the scalars as hi + lo pairs):
+// half the all-reduce bytes; measured drift DESIGN.md section 6 (1.8e-7 with one rank, 1.5e-6
+// with eight: each rank's partial is rounded before the cross-rank cancellation), so it is
+// opt-in: 1 = any row-shard exchange, -1 = RCCL communicators only, 0 (default) = fp64.  The
+// exact-gradient refresh is always fp64.
+bool xch_f32(const bpgl_ctx* c) {
+    return c->rows && (c->xch32 > 0 || (c->xch32 < 0 && c->comm && !c->external));
+}
 OnePassArgs op_tail_args(const bpgl_ctx* c) {
     OnePassArgs o = c->op;
     if (c->rows) {
@@ -1068,7 +1072,8 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         return 0;
     }
     if (!strcmp(key, "exchange_fp32")) {
-        c->xch32 = value != 0;
+        if (value < -1 || value > 1) return fail(BPGL_E_ARG, "exchange_fp32 must be -1, 0 or 1");
+        c->xch32 = (int)value;
         drop_graphs(c);
         c->solver = false;
         return 0;

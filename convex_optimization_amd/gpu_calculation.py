@@ -300,12 +300,16 @@ class GPU_Calculation:
         with self._on_stream():
             N.check(N.lib().bpgl_solver_phase(self._ctx, int(phase)), "bpgl_solver_phase")
 
-    def exchange_buffer(self):
+    def exchange_buffer(self, fp32=False):
         """Device view of the per-iteration exchange (lives in the scratch): column shards
-        [s23 (m) | sum|Bx| | sum|x| | err slot per rank]; row shards [U (w_pad) | r.s23 | s23.s23]."""
+        [s23 (m) | sum|Bx| | sum|x| | err slot per rank]; row shards [U (w_pad) | r.s23 | s23.s23].
+        ``fp32``: the row shards' fp32 format of phases 0/1 ("exchange_fp32" = 1), w_pad + 4
+        float32 [U | r.s23 hi, lo | s23.s23 hi, lo] at the same address."""
         cnt = ctypes.c_int64()
         addr = N.lib().bpgl_solver_exchange_buffer(self._ctx, ctypes.byref(cnt))
         off = (addr - self._scratch.data_ptr()) // 8
+        if fp32:
+            return self._scratch.view(torch.float32)[2 * off:2 * off + cnt.value + 2]
         return self._scratch[off:off + cnt.value]
 
     def set_tuning(self, key, value):

@@ -126,7 +126,9 @@ int bpgl_comm_init(bpgl_ctx* ctx, const void* unique_id128, int rank, int nranks
  * q holds rows [m_q, m_{q+1}) of A (the context's m is its row count, n_local the
  * full width), b and the residual are local, x is replicated.  Row shards run the
  * one-pass iteration (A read once per iteration): per iteration one all-reduce
- * (SUM) of w_pad + 2 fp64 [A^T A D | r.s23 | s23.s23]; bpgl_diag_ata and every
+ * (SUM) of [A^T A D | r.s23 | s23.s23] -- w_pad + 2 fp64, or (opt-in tuning key
+ * "exchange_fp32") w_pad + 4 fp32 (U rounded, the scalars as hi + lo pairs);
+ * bpgl_diag_ata and every
  * exact gradient refresh all-reduce w_pad values.  There is no reference
  * counterpart: the reference shards columns only (cpu_calculation.py:23-27).
  */
@@ -145,7 +147,10 @@ int bpgl_set_shard(bpgl_ctx* ctx, int mode);
 /* Row shards (count = w_pad + 2): the same two phases per iteration; in
  * addition the exact gradient g = A^T r is exchanged by phase 2 (this rank's
  * A_q^T r_q into the exchange buffer), the caller's sum, and phase 3 -- after
- * bpgl_solver_reset and again every "onepass_refresh" iterations. */
+ * bpgl_solver_reset and again every "onepass_refresh" iterations.  With the
+ * tuning key "exchange_fp32" = 1 phases 0/1 exchange w_pad + 4 fp32 at the same
+ * address instead: [U (w_pad) | r.s23 hi, lo | s23.s23 hi, lo]; phases 2/3 stay
+ * fp64. */
 int bpgl_set_ranks(bpgl_ctx* ctx, int rank, int nranks);
 int bpgl_solver_phase(bpgl_ctx* ctx, int phase);
 double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
@@ -215,6 +220,9 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
  *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "fused" (default 0): the two-launch fused iteration.
+ *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for
+ *   a caller-side exchange): row shards' per-iteration exchange in fp32 -- half the
+ *   bytes, x within 2e-7 (1 rank) to 1.5e-6 (8 ranks) of the fp64 exchange.
  * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the
  * number of (row chunk x column segment) tiles per two-pass launch (default
  * 1024 for fp32 A, 512 for fp64 / bf16). */
