@@ -425,12 +425,49 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
             p.r[k] = ax - p.b[k];
         }
     }
-    // columns: tiles of 64 (lane = column); the 4 waves split the row-group partials of U
-    // (q = wave, wave + 4, ...), wave 0 adds the 4 sums in a fixed order and runs the shrink
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ double ured[kWaves][64];
     double abx = 0.0, ax1 = 0.0, err = 0.0;
     const long long ntile = (p.wp + 63) / 64;
+    // the shrink of one column j with U_j already summed (u); accumulates this lane's partials
+    auto shrink_col = [&](long long j, double g, double u, double xj, double dold, double dg, double rc) {
+        if (UPDATE) {
+            g += gamma * u;
+            o.G[j] = g;
+        }
+        p.g[j] = g;
+        double Dj = 0.0;
+        if (j < p.w) {
+            if (UPDATE) {
+                xj += gamma * dold;
+                p.x[j] = xj;
+            }
+            const double rx = dg * xj - g;                        // lasso.py:114
+            const double bx = rc * soft_thr(rx, p.mu);            // lasso.py:115-117
+            Dj = bx - xj;                                         // lasso.py:119
+            abx += fabs(bx);
+            ax1 += fabs(xj);
+            const double e = fabs(g - proj(g - xj, -p.mu, p.mu)); // cpu_calculation.py:15-20
+            err = (e > err || e != e) ? e : err;
+        }
+        p.D[j] = Dj;
+    };
+    if (o.ngroups == 1) {
+        // row shards (U already summed over ranks): every wave takes its own 64-column tiles
+        for (long long tile = (long long)blockIdx.x * kWaves + wave; tile < ntile;
+             tile += (long long)gridDim.x * kWaves) {
+            const long long j = tile * 64 + lane;
+            if (j >= p.wp) continue;
+            const bool col = j < p.w;
+            const double g = o.G[j];
+            const double u = !UPDATE ? 0.0 : o.Uf ? (double)o.Uf[j] : o.Us[j];
+            const double xj = col ? p.x[j] : 0.0, dold = (UPDATE && col) ? p.D[j] : 0.0;
+            const double dg = col ? p.diag[j] : 0.0, rc = col ? p.rec[j] : 0.0;
+            shrink_col(j, g, u, xj, dold, dg, rc);
+        }
+    } else
+    // one rank: tiles of 64 (lane = column); the 4 waves split the row-group partials of U
+    // (q = wave, wave + 4, ...), wave 0 adds the 4 sums in a fixed order and runs the shrink
     for (long long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {   // block-uniform
         const long long j = tile * 64 + lane;
         const bool ok = j < p.wp;
@@ -460,34 +497,25 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
             __syncthreads();
         }
         if (wave == 0 && ok) {
-            if (UPDATE) {
-                g += gamma * (((ured[0][lane] + ured[1][lane]) + ured[2][lane]) + ured[3][lane]);
-                o.G[j] = g;
-            }
-            p.g[j] = g;
-            double Dj = 0.0;
-            if (col) {
-                if (UPDATE) {
-                    xj += gamma * dold;
-                    p.x[j] = xj;
-                }
-                const double rx = dg * xj - g;                        // lasso.py:114
-                const double bx = rc * soft_thr(rx, p.mu);            // lasso.py:115-117
-                Dj = bx - xj;                                         // lasso.py:119
-                abx += fabs(bx);
-                ax1 += fabs(xj);
-                const double e = fabs(g - proj(g - xj, -p.mu, p.mu)); // cpu_calculation.py:15-20
-                err = (e > err || e != e) ? e : err;
-            }
-            p.D[j] = Dj;
+            const double u = UPDATE ? ((ured[0][lane] + ured[1][lane]) + ured[2][lane]) + ured[3][lane] : 0.0;
+            shrink_col(j, g, u, xj, dold, dg, rc);
         }
         if (UPDATE) __syncthreads();   // ured is rewritten by the next tile
     }
-    if (wave == 0) {
-        abx = wave_sum(abx);
-        ax1 = wave_sum(ax1);
-        err = wave_max(err);
-        if (lane == 0) {
+    // block partials: wave sums, then the 4 waves in a fixed order (waves 1-3 hold zeros on the
+    // one-rank path, where only wave 0 runs the shrink: adding them changes no bit)
+    abx = wave_sum(abx);
+    ax1 = wave_sum(ax1);
+    err = wave_max(err);
+    __shared__ double wred[3][kWaves];
+    if (lane == 0) { wred[0][wave] = abx; wred[1][wave] = ax1; wred[2][wave] = err; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        abx = ((wred[0][0] + wred[0][1]) + wred[0][2]) + wred[0][3];
+        ax1 = ((wred[1][0] + wred[1][1]) + wred[1][2]) + wred[1][3];
+        err = wred[2][0];
+        for (int q = 1; q < kWaves; ++q) err = (wred[2][q] > err || wred[2][q] != wred[2][q]) ? wred[2][q] : err;
+        {
             double* dst = p.parts + 4ll * blockIdx.x;
             dst[0] = abx;
             dst[1] = ax1;
