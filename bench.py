@@ -237,9 +237,22 @@ def cpu_baseline(gc, b, mu, seconds):
     t0 = time.perf_counter()
     oracle.run(A, bh, mu, gc.Block, iters, nthreads=threads)
     el = time.perf_counter() - t0
-    return {"value": iters / el, "unit": "iters/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/bpgl_oracle.c oracle_run, {iters} iterations from x=0 on the same "
-                      f"{H}x{gc.Block * W} fp32 A and b, {threads} OpenMP threads (fp64 arithmetic)"}
+    out = {"value": iters / el, "unit": "iters/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/bpgl_oracle.c oracle_run, {iters} iterations from x=0 on the same "
+                     f"{H}x{gc.Block * W} fp32 A and b, {threads} OpenMP threads (fp64 arithmetic)"}
+    # SURVEY 8d also asks for the numpy restatement (OpenBLAS GEMVs, fp64) beside it: a few
+    # iterations, bounded to about a third of the C sample's time
+    A64 = A.astype(np.float64)
+    t0 = time.perf_counter()
+    oracle.run_numpy(A64, bh, mu, gc.Block, 1)
+    per = time.perf_counter() - t0
+    n_np = int(max(2, min(50, seconds / 3 / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    oracle.run_numpy(A64, bh, mu, gc.Block, n_np)
+    out["numpy_fp64"] = {"value": n_np / (time.perf_counter() - t0), "unit": "iters/s",
+                         "threads": "OpenBLAS default (OMP_NUM_THREADS=" + os.environ.get("OMP_NUM_THREADS", "unset") + ")",
+                         "sample": f"oracle.run_numpy, {n_np} iterations from x=0 on the same A (as fp64)"}
+    return out
 
 
 def vendor_yardstick(gc, reps=20):
