@@ -105,8 +105,8 @@ struct bpgl_ctx {
 namespace {
 
 void drop_graphs(bpgl_ctx* c) {
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-    if (c->gexec_k) { hipGraphExecDestroy(c->gexec_k); c->gexec_k = nullptr; }
+    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    if (c->gexec_k) { (void)hipGraphExecDestroy(c->gexec_k); c->gexec_k = nullptr; }
 }
 
 void geometry(bpgl_ctx* c) {
@@ -419,7 +419,7 @@ void ev_record(bpgl_ctx* c, int64_t it, int kind, int end) {
         if (hipEventCreate(&e) != hipSuccess) return;
         c->evs.push_back(e);
     }
-    hipEventRecord(c->evs[idx], c->stream);
+    (void)hipEventRecord(c->evs[idx], c->stream);
     c->kind_used[kind] = true;
 }
 
@@ -634,11 +634,11 @@ int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_lo
 
 void bpgl_destroy(bpgl_ctx* c) {
     if (!c) return;
-    hipSetDevice(c->device);
+    (void)hipSetDevice(c->device);   // destroy path: nothing to report to
     drop_graphs(c);
-    for (auto e : c->evs) hipEventDestroy(e);
+    for (auto e : c->evs) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
-    if (c->own_stream) hipStreamDestroy(c->stream);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -947,10 +947,10 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
             rc = 0;
             for (int k = 0; k < iters && !rc; ++k) rc = enqueue_iteration(c, 0);
             hipError_t ec = hipStreamEndCapture(c->stream, &graph);
-            if (rc) { if (graph) hipGraphDestroy(graph); c->timing = was_timing; return rc; }
+            if (rc) { if (graph) (void)hipGraphDestroy(graph); c->timing = was_timing; return rc; }
             if (ec != hipSuccess) { c->timing = was_timing; return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec)); }
             hipError_t ei = hipGraphInstantiate(variant == 0 ? &c->gexec : &c->gexec_k, graph, nullptr, nullptr, 0);
-            hipGraphDestroy(graph);
+            (void)hipGraphDestroy(graph);
             if (ei != hipSuccess) { c->timing = was_timing; return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei)); }
         }
         c->timing = was_timing;

@@ -126,7 +126,7 @@ void panel_ev(bpgl_panel* c, int64_t it, int kind, int end) {
         if (hipEventCreate(&e) != hipSuccess) return;
         c->evs.push_back(e);
     }
-    hipEventRecord(c->evs[idx], c->stream);
+    (void)hipEventRecord(c->evs[idx], c->stream);
 }
 int panel_iteration(bpgl_panel* c, int64_t it) {
     int rc;
@@ -211,10 +211,10 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
 
 void bpgl_panel_destroy(bpgl_panel* c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->gexec) hipGraphExecDestroy(c->gexec);
-    for (auto e : c->evs) hipEventDestroy(e);
-    if (c->own_stream) hipStreamDestroy(c->stream);
+    (void)hipSetDevice(c->device);   // destroy path: nothing to report to
+    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    for (auto e : c->evs) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -264,7 +264,7 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     c->bound = true;
     c->have_diag = false;
     c->solver = false;
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
     return 0;
 }
 
@@ -322,7 +322,7 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     p.rec_len = err_iter ? record_len : 0;
     hipLaunchKernelGGL(k_panel_reset_state, dim3(1), dim3(64), 0, c->stream, c->p);
     LAUNCH_CHECK("k_panel_reset_state");
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
     if (use_graph) {
         hipGraph_t graph = nullptr;
         const bool was = c->timing;
@@ -332,10 +332,10 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
         for (int k = 0; k < kGraphIters && !rc; ++k) rc = panel_iteration(c, 0);
         hipError_t ec = hipStreamEndCapture(c->stream, &graph);
         c->timing = was;
-        if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
+        if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
         if (ec != hipSuccess) return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
         hipError_t ei = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
+        (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
     }
     c->solver = true;
@@ -428,7 +428,7 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else {
         return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     }
-    if (c->gexec) { hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
     return 0;
 }
 
