@@ -148,7 +148,8 @@ void geometry(bpgl_ctx* c) {
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opUs, opPG, opS, total;
+    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opUs, opPG, opS, opABE,
+        total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -173,6 +174,7 @@ Layout layout(const bpgl_ctx* c) {
     L.opUs = k.take(op ? 8 * (int64_t)c->op_ngroups * c->wp : 0);
     L.opPG = k.take(op ? 8 * c->m * c->op_SB : 0);
     L.opS = k.take(op && c->rows ? 8 * c->m : 0);
+    L.opABE = k.take(op && c->rows ? 8 * 4 : 0);
     L.total = k.off;
     return L;
 }
@@ -486,7 +488,7 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
         ev_record(c, it, 3, 0);
         float* xf = xch_f32(c) ? reinterpret_cast<float*>(c->p.comm) : nullptr;
         hipLaunchKernelGGL(k_onepass_fold, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024)),
-                           dim3(kThreads), 0, c->stream, c->p, c->op, c->p.comm, xf);
+                           dim3(kThreads), 0, c->stream, op_params(c), c->op, c->p.comm, xf);
         LAUNCH_CHECK("k_onepass_fold");
         ev_record(c, it, 3, 1);
         if (c->comm) {
@@ -500,13 +502,9 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
             ev_record(c, it, 4, 1);
         }
     }
-    if ((phase == 0 && !c->external) || (phase == 1 && c->external)) {
-        ev_record(c, it, 5, 0);
-        const float* pf = xch_f32(c) ? reinterpret_cast<const float*>(c->p.comm) + c->wp : nullptr;
-        hipLaunchKernelGGL(k_linesearch, dim3(1), dim3(kThreads), 0, c->stream, ls, 1, pf);
-        LAUNCH_CHECK("k_linesearch");
-        ev_record(c, it, 5, 1);
-    }
+    // the line search runs at the head of k_onepass_tail (o.abe: the fold pre-summed the shrink
+    // partials; [r.s23, s23.s23] come from the exchange buffer)
+    (void)ls;
     if (phase == 1) {
         ev_record(c, it, 6, 0);
         if ((rc = onepass_tail<true>(c))) return rc;
@@ -720,7 +718,8 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
         c->op.ngroups = c->op_ngroups;
         c->op.R = c->op_R;
         c->op.xl = c->op_xl;
-        c->op.ls = c->rows ? 0 : 1;   // row shards: the line search follows the all-reduce
+        c->op.ls = c->rows ? 0 : 1;   // row shards: the line search follows the all-reduce (in the tail)
+        c->op.abe = c->rows ? (double*)(s + L.opABE) : nullptr;
         c->op.cache_permille = c->op_cache;
     }
     HIP_TRY(hipSetDevice(c->device));

@@ -57,6 +57,7 @@ struct OnePassArgs {
     int ls;                      // 1: the last row group to finish runs the line search (one rank)
     int cache_permille;          // share of each group's rows read last with cache-allocating loads
     const float* Uf;             // row shards, fp32 exchange: the all-reduced U (read instead of Us)
+    double* abe;                 // row shards: [sum|Bx|, sum|x|, max err] of the last shrink (k_onepass_fold)
 };
 
 typedef unsigned long long op_u64;
@@ -381,6 +382,14 @@ __global__ __launch_bounds__(kThreads) void k_onepass_fold(Params p, OnePassArgs
         if (outf) outf[j] = (float)acc;
         else out[j] = acc;
     }
+    // block 0 also folds the last shrink's per-block partials (identical on every rank: x, g and
+    // D are replicated) for the line search at the head of k_onepass_tail -- the fold k_linesearch
+    // ran, in the same order (p.nparts = the tail's grid)
+    if (o.abe && blockIdx.x == 0) {   // block-uniform
+        double a, b, e;
+        fold_parts(p, p.nparts, a, b, e);
+        if (threadIdx.x == 0) { o.abe[0] = a; o.abe[1] = b; o.abe[2] = e; }
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         double rs = 0.0, ss = 0.0;
         for (int q = 0; q < o.ngroups; ++q) { rs += p.parts2[2ll * q]; ss += p.parts2[2ll * q + 1]; }
@@ -415,7 +424,28 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
         p.st->op_ran = 0;
     }
     if (p.st->done) return;
-    const double gamma = UPDATE ? p.st->gamma : 0.0;
+    double gamma = UPDATE ? p.st->gamma : 0.0;
+    if (UPDATE && o.abe) {
+        // row shards: the line search (lasso.py:129-150) on the all-reduced [r.s23, s23.s23] and the
+        // fold's shrink sums, computed identically by every block (the same inputs, the same
+        // arithmetic as k_linesearch: rs and ss are the sums of one value each).  One feature
+        // block: the stop rule is err < err_bound in this iteration (block_cnt never carries).
+        // Block 0 records the state (finish_step); a block that finds the rule fired updates nothing.
+        double rs, ss;
+        if (o.Uf) {
+            rs = (double)o.Uf[p.wp] + (double)o.Uf[p.wp + 1];
+            ss = (double)o.Uf[p.wp + 2] + (double)o.Uf[p.wp + 3];
+        } else {
+            rs = o.Us[p.wp];
+            ss = o.Us[p.wp + 1];
+        }
+        const double a = o.abe[0], b = o.abe[1], e = o.abe[2];
+        const double r1 = rs + p.mu * (a - b);
+        gamma = (ss == 0.0) ? 0.0 : proj(-r1 / ss, 0.0, 1.0);
+        const bool stop = p.err_bound >= 0.0 && e < p.err_bound;
+        if (blockIdx.x == 0 && threadIdx.x == 0) finish_step(p, rs, ss, a, b, e);
+        if (stop) return;   // block-uniform
+    }
     const long long stride = (long long)gridDim.x * kThreads;
     const long long k0 = (long long)blockIdx.x * kThreads + threadIdx.x;
     if (UPDATE) {
