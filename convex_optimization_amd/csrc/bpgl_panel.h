@@ -757,7 +757,10 @@ __device__ __forceinline__ void panel_bump_t(const PanelParams& p, bool pending)
 // Work units: u < ux -> 8 consecutive x elements ([k][w], 16-B Dh (+ Dl when DS = 2) loads);
 // ux <= u < ux + ur -> 4 consecutive residual rows ([k][m]).  Also bumps t.  k*w and k*m <
 // 2^31 (checked at create), so the index math is 32-bit.
-template <int DS>
+// NB1 (one feature block): R_j += gamma_j S_j directly -- R = Ax - B with a single block, so Ax
+// and B need not be read or written (28 instead of 44 bytes per residual element); Ax is then not
+// maintained (nothing reads it with one block).
+template <int DS, bool NB1>
 __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
     const int mb = (int)p.st->cur_mb;   // p.st->t is advanced by block 0 of this launch
     const long long nx = (long long)p.k * p.w, nr = (long long)p.k * p.m;
@@ -790,22 +793,34 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
             const unsigned v = u - ux;
             const long long e = 4ll * v;
             const double g = p.gamma[v / m4];
-            double* ap = p.Ax + (long long)mb * nr + e;
-            double a[4], acc[4], r[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) a[q] = ap[q] + g * p.S[e + q];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ap[q] = a[q];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = mb == 0 ? a[q] : p.Ax[e + q];
-            for (int b = 1; b < p.nblock; ++b)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[q] += b == mb ? a[q] : p.Ax[(long long)b * nr + e + q];
+            double r[4];
             __bf16 hi[4], lo[4];
+            if constexpr (NB1) {
+                const double2 r01 = *reinterpret_cast<const double2*>(p.R + e);
+                const double2 r23 = *reinterpret_cast<const double2*>(p.R + e + 2);
+                const double2 s01 = *reinterpret_cast<const double2*>(p.S + e);
+                const double2 s23 = *reinterpret_cast<const double2*>(p.S + e + 2);
+                r[0] = r01.x + g * s01.x; r[1] = r01.y + g * s01.y;
+                r[2] = r23.x + g * s23.x; r[3] = r23.y + g * s23.y;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                r[q] = acc[q] - p.B[e + q];
-                split_bf16(r[q], hi[q], lo[q]);
+                for (int q = 0; q < 4; ++q) split_bf16(r[q], hi[q], lo[q]);
+            } else {
+                double* ap = p.Ax + (long long)mb * nr + e;
+                double a[4], acc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = ap[q] + g * p.S[e + q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ap[q] = a[q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = mb == 0 ? a[q] : p.Ax[e + q];
+                for (int b = 1; b < p.nblock; ++b)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] += b == mb ? a[q] : p.Ax[(long long)b * nr + e + q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    r[q] = acc[q] - p.B[e + q];
+                    split_bf16(r[q], hi[q], lo[q]);
+                }
             }
             wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
             wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));

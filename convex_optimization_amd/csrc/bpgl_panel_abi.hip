@@ -146,8 +146,14 @@ int panel_iteration(bpgl_panel* c, int64_t it) {
     } else {
         const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
         const dim3 ug((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192));
-        if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_update<1>, ug, dim3(kThreads), 0, c->stream, c->p);
-        else hipLaunchKernelGGL(k_panel_update<2>, ug, dim3(kThreads), 0, c->stream, c->p);
+        const bool nb1 = c->nblock == 1;
+        if (c->dsplit == 1) {
+            if (nb1) hipLaunchKernelGGL((k_panel_update<1, true>), ug, dim3(kThreads), 0, c->stream, c->p);
+            else hipLaunchKernelGGL((k_panel_update<1, false>), ug, dim3(kThreads), 0, c->stream, c->p);
+        } else {
+            if (nb1) hipLaunchKernelGGL((k_panel_update<2, true>), ug, dim3(kThreads), 0, c->stream, c->p);
+            else hipLaunchKernelGGL((k_panel_update<2, false>), ug, dim3(kThreads), 0, c->stream, c->p);
+        }
     }
     LAUNCH_CHECK("k_panel_update");
     panel_ev(c, it, 4, 1);
