@@ -8,17 +8,32 @@ HBM before the timed region.
 
   N = 1 : BASELINE configs[1]  m=8192 n=65536 fp32 A, one feature block.
   N > 1 : BASELINE configs[2]  m=8192 n=65536*N (n = 524288 at N = 8), weak scaling:
-          every GPU holds 2 GiB of A, the per-GPU work of N = 1.  Default
-          (--shard rows): GPU g holds rows [g m/N, (g+1) m/N) of A (all columns),
-          streams them once per iteration (k_onepass), and ONE RCCL all-reduce of
-          n + 2 fp64 values per iteration carries U = A^T A D and the line-search
-          dot products.  --shard columns: the reference's column split (every GPU
-          an 8192 x 65536 column shard), two passes over A per iteration and one
-          all-reduce of m + 2 + N fp64 (the residual side).  The work unit is one
-          "block-iteration" = one iteration's worth of an 8192 x 65536 fp32 matrix
-          (the whole configs[1] matrix), so value = N x global iterations/s.
-          A strong-scaling measurement (the fixed 8192 x 65536 matrix split
-          N ways the same way) is reported beside it under "strong".
+          every GPU holds 2 GiB of A, the per-GPU work of N = 1.  The split
+          (--shard auto) follows the cost model of DESIGN.md section 6: one feature
+          block -> rows (GPU g holds rows [g m/N, (g+1) m/N) of A, all columns,
+          streams them once per iteration with k_onepass, and ONE RCCL all-reduce of
+          n + 3 fp64 values per iteration carries U = A^T A D, the line-search dot
+          products and the failure flag); several feature blocks -> columns (the
+          reference's P-way split, cpu_calculation.py:23-27: two passes over A per
+          iteration and one all-reduce of m + 2 + N fp64 on the residual side).
+          The work unit is one "block-iteration" = one iteration's worth of an
+          8192 x 65536 fp32 matrix (the whole configs[1] matrix), so value = N x
+          global iterations/s.  A strong-scaling measurement (the fixed 8192 x 65536
+          matrix split N ways the same way) is reported beside it under "strong".
+  --config 2: configs[2]'s own problem (m=8192 n=524288) split over the N GPUs
+          (strong scaling; at N = 1 the whole 16 GiB matrix on one GPU).
+  --config 3 / 4: configs[3] (1048576 x 4096 fp32) / configs[4] (k = 128
+          right-hand sides on bf16 A), one GPU.
+
+Timing (every workload): W untimed warm-up iterations; an eager window of
+max(K, 512) iterations with HIP events around every kernel on the solver stream
+(the per-kernel averages behind `roofline`, and the clock ramp of a fresh box);
+then `--windows` (default 5) windows of exactly K graph-replayed iterations, each
+bracketed by a barrier and device synchronisation, max over ranks.  value and
+ms_per_step come from the median window, with the one-pass exact-gradient refresh
+(one A^T r pass every 256 iterations) folded in at its amortised rate: a window's
+time minus the refreshes it happened to contain, plus K/256 refreshes, each at the
+event-timed refresh cost.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
@@ -70,16 +85,16 @@ def alg_bytes_rowpass(m, w, sa=4):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
-                    help="BASELINE.json configs[K]: 1 = 8192x65536 fp32 (default), 2 = its column-sharded "
-                         "multi-GPU form, 3 = 1048576x4096 fp32, 4 = k=128 right-hand sides on bf16 A")
+                    help="BASELINE.json configs[K]: 1 = 8192x65536 fp32 (default; weak scaling over N GPUs), "
+                         "2 = 8192x524288 fp32 split over the N GPUs (strong), 3 = 1048576x4096 fp32, "
+                         "4 = k=128 right-hand sides on bf16 A")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=256,
-                    help="timed iterations (default 256: with the default warmup the window holds exactly one "
-                         "exact-gradient refresh of the one-pass iteration, i.e. its amortised cost)")
+                    help="iterations per timed window (default 256)")
     ap.add_argument("--warmup", type=int, default=200,
-                    help="untimed iterations before the window (default 200: the first ~100 ms of steady load "
-                         "run 1-7 %% slower on a fresh box -- measured configs[1] 2912 -> 2939 it/s, configs[4] "
-                         "1849 -> 1976 it/s going from 20/10 to 300/100 warmup iterations)")
+                    help="untimed iterations before the windows (default 200)")
+    ap.add_argument("--windows", type=int, default=5,
+                    help="timed windows of exactly --steps iterations; value uses the median (default 5)")
     ap.add_argument("--m", type=int, default=M)
     ap.add_argument("--n-per-gpu", type=int, default=N_PER_GPU)
     ap.add_argument("--block", type=int, default=1)
@@ -96,12 +111,13 @@ def parse():
                     help="permille of each one-pass row group read with cache-allocating loads (-1: library default)")
     ap.add_argument("--comm", action="store_true",
                     help="attach an RCCL communicator even at N = 1 (runs the sharded/all-reduce leg)")
-    ap.add_argument("--shard", default="rows", choices=["rows", "columns"],
-                    help="multi-GPU split (N > 1, or N = 1 with --comm): rows (default; one pass over A, "
-                         "all-reduce of n + 2) or columns (the reference's split; two passes, all-reduce of m + 2 + N)")
+    ap.add_argument("--shard", default="auto", choices=["auto", "rows", "columns"],
+                    help="multi-GPU split (N > 1, or N = 1 with --comm): auto (default: rows for one feature block, "
+                         "columns for several -- the cost model of DESIGN.md section 6), rows (one pass over A, "
+                         "all-reduce of n + 3) or columns (the reference's split; two passes, all-reduce of m + 2 + N)")
     ap.add_argument("--exchange-fp32", type=int, default=0, choices=[0, 1],
-                    help="RCCL row shards: the per-iteration all-reduce of [U | r.s23 | s23.s23] in fp32 (1, opt-in: "
-                         "half the bytes, x within ~1e-6 of the fp64 exchange) or fp64 (0, default)")
+                    help="RCCL row shards: the per-iteration all-reduce of [U | r.s23 | s23.s23 | failed] in fp32 "
+                         "(1, opt-in: half the bytes, x within ~1e-6 of the fp64 exchange) or fp64 (0, default)")
     ap.add_argument("--rhs", type=int, default=1,
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
@@ -117,12 +133,41 @@ def parse():
                     help="panel path, one block: apply x += gamma D in the next pass-1 epilogue (1) or in the "
                          "update kernel (0); -1: library default")
     a = ap.parse_args()
-    if a.config == 3:
+    a.strong_total = False
+    if a.config == 2:
+        world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
+        a.m, a.strong_total = 8192, True
+        if 524288 % world:
+            raise SystemExit("--config 2 splits n = 524288 over the GPUs: N must divide it")
+        a.n_per_gpu = 524288 // world
+    elif a.config == 3:
         a.m, a.n_per_gpu = 1048576, 4096
         a.steps, a.warmup = min(a.steps, 30), min(a.warmup, 40)   # 2.7 ms per iteration
     elif a.config == 4:
         a.rhs = 128
+    if a.shard == "auto":
+        a.shard = "rows" if a.block == 1 else "columns"
+    a.windows = max(1, a.windows)
     return a
+
+
+def workload_label(args, G, m, n_total, ml, w, rows):
+    """configs[K] label from the actual shape (BASELINE.json configs)."""
+    if args.config == 2 or (m, n_total) == (8192, 524288):
+        name = "configs[2]"
+    elif args.config == 3 or (m, n_total) == (1048576, 4096):
+        name = "configs[3]"
+    elif (m, n_total) == (8192, 65536) and G == 1:
+        name = "configs[1]"
+    elif m == 8192 and n_total == 65536 * G:
+        name = "configs[2]-style weak scaling"
+    else:
+        name = "custom"
+    s = f"{name}: m={m} n={n_total} {args.type} A, {args.block} feature block(s), {G} GPU(s)"
+    if G > 1:
+        s += (f", row-sharded {ml} rows/GPU, one RCCL all-reduce of n+3 fp64 per iteration" if rows else
+              f", column-sharded {w} cols/GPU, one RCCL all-reduce of m+2+N fp64 per iteration")
+    return s
 
 
 class Ctx:
@@ -157,6 +202,15 @@ class Ctx:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t[0])
 
+    def gather(self, v):
+        """every rank's float, in rank order (gloo)"""
+        if self.world == 1:
+            return [float(v)]
+        import torch
+        out = [torch.zeros(1, dtype=torch.float64) for _ in range(self.world)]
+        self.dist.all_gather(out, torch.tensor([float(v)], dtype=torch.float64))
+        return [float(t[0]) for t in out]
+
 
 def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, shard="rows"):
     import torch
@@ -176,23 +230,28 @@ def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, sha
     return gc, b, mu
 
 
-def timed_window(ctx, gc, steps, graph):
-    """barrier + sync, `steps` iterations, sync + barrier; returns max-over-ranks seconds."""
-    import torch
-    gc.set_kernel_timing(not graph)
+def timed_window(ctx, sync, step, steps):
+    """barrier + sync, exactly `steps` iterations, sync + barrier; max-over-ranks seconds."""
     ctx.barrier()
-    torch.cuda.synchronize()
-    gc.stream.synchronize()
+    sync()
     t0 = time.perf_counter()
-    gc.solver_step(steps)
-    gc.stream.synchronize()
-    torch.cuda.synchronize()
+    step(steps)
+    sync()
     t1 = time.perf_counter()
     ctx.barrier()
     return ctx.max(t1 - t0)
 
 
+def median(v):
+    v = sorted(v)
+    k = len(v)
+    return v[k // 2] if k % 2 else 0.5 * (v[k // 2 - 1] + v[k // 2])
+
+
 def measure(ctx, args, m, n_total):
+    """W warm-up iterations, an eager window with per-kernel HIP events (max(K, 512) iterations),
+    then `windows` graph windows of exactly K iterations (see the module docstring)."""
+    import torch
     gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard)
     gc.set_tuning("fused", args.fused)
     gc.set_tuning("onepass", args.onepass)
@@ -201,24 +260,87 @@ def measure(ctx, args, m, n_total):
     gc.set_tuning("onepass_variant", args.onepass_variant)
     if args.onepass_cache >= 0:
         gc.set_tuning("onepass_cache_permille", args.onepass_cache)
-    # graph replay needs per-kernel events off; timing mode launches eagerly with
-    # HIP events around every kernel on the solver stream.
+
+    def sync():
+        gc.stream.synchronize()
+        torch.cuda.synchronize()
+
     gc.solver_reset(b, mu, use_graph=True)
     gc.solver_step(args.warmup)
-    gc.stream.synchronize()
-    el_graph = timed_window(ctx, gc, args.steps, graph=True)
-    st = gc.solver_status()
-    gc.solver_reset(b, mu, use_graph=False)
-    gc.solver_step(args.warmup)
-    gc.stream.synchronize()
-    el_ev = timed_window(ctx, gc, args.steps, graph=False)
+    sync()
+    # eager window: kernel averages (events on the solver stream) + clock ramp
+    n_ev = max(args.steps, 512)
+    gc.set_kernel_timing(True)
+    r0 = gc.solver_stat("refreshes")
+    el_ev = timed_window(ctx, sync, gc.solver_step, n_ev)
+    n_ref_ev = gc.solver_stat("refreshes") - r0
     times, samples = gc.kernel_times()
     gc.set_kernel_timing(False)
-    return dict(gc=gc, el_graph=el_graph, el_events=el_ev, kernel_ms=times, samples=samples, status=st,
-                w_local=gc.MAT_WIDTH, m_local=gc.MAT_HEIGHT, b=b, mu=mu)
+    refresh_ms = times["refresh"] * samples / n_ref_ev if n_ref_ev else 0.0
+    period = gc.solver_stat("refresh_period")
+    refresh_ms = ctx.max(refresh_ms)
+    st = gc.solver_status()   # completes any iteration a failed one-pass launch lost (outside the windows)
+    # graph windows; after each, the status call (outside the window) would re-run iterations a
+    # failed one-pass launch lost -- such a window did not do its K iterations and is dropped
+    wins = []
+    for _ in range(args.windows):
+        r0 = gc.solver_stat("refreshes")
+        rec0 = gc.solver_stat("fallbacks") + gc.solver_stat("retries")
+        el = timed_window(ctx, sync, gc.solver_step, args.steps)
+        n_ref = ctx.max(gc.solver_stat("refreshes") - r0)
+        st = gc.solver_status()
+        lost = ctx.max(gc.solver_stat("fallbacks") + gc.solver_stat("retries") - rec0) > 0
+        adj = el - n_ref * refresh_ms * 1e-3 + (args.steps / period * refresh_ms * 1e-3 if period else 0.0)
+        wins.append({"s": el, "refreshes": int(n_ref), "s_amortised": adj, "lost_iterations": bool(lost)})
+    if all(w["lost_iterations"] for w in wins):
+        raise SystemExit("every timed window lost one-pass iterations (another process holds CUs?)")
+    assert st["iters"] == args.warmup + n_ev + args.windows * args.steps or st["stopped"], st
+    return dict(gc=gc, windows=wins, el_events=el_ev, n_events=n_ev, kernel_ms=times, samples=samples, status=st,
+                refresh_ms=refresh_ms, refresh_period=period, w_local=gc.MAT_WIDTH, m_local=gc.MAT_HEIGHT,
+                b=b, mu=mu, fallbacks=gc.solver_stat("fallbacks"), retries=gc.solver_stat("retries"))
 
 
-def cpu_baseline(gc, b, mu, seconds):
+def host_cores():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS when set (the GPU boxes give each job a share of a large host; os.cpu_count()
+    counts the whole host).  Returns (threads, description)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except Exception:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    n = aff
+    if quota:
+        n = min(n, quota)
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return n, {"threads": n, "os_cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+               "OMP_NUM_THREADS": omp, "model": model}
+
+
+def cpu_pool_leg(cores):
+    """The reference's own Pool-parallel CPU loop at configs[0] (oracle/pool_baseline.py).  Run
+    before this process touches the GPU: the pool forks."""
+    try:
+        from oracle.pool_baseline import pool_baseline
+        return pool_baseline(cores)
+    except Exception as e:  # a reported baseline, never a reason to lose the GPU line
+        return {"error": repr(e)}
+
+
+def cpu_baseline(gc, b, mu, seconds, cores, cpu_info, share_note=""):
     """The oracle (C restatement of the reference iteration) on this host's cores,
     bounded sample of the same workload: the same A (copied back to host fp32),
     as many iterations as fit in about `seconds` of CPU time."""
@@ -229,7 +351,7 @@ def cpu_baseline(gc, b, mu, seconds):
     A = gc.A_b_gpu.permute(1, 0, 2).reshape(H, gc.Block * W).cpu().numpy()
     A = np.ascontiguousarray(A)
     bh = b.cpu().numpy()
-    threads = min(16, os.cpu_count() or 1)
+    threads = cores
     t0 = time.perf_counter()
     oracle.run(A, bh, mu, gc.Block, 2, nthreads=threads)
     per = (time.perf_counter() - t0) / 2
@@ -239,7 +361,8 @@ def cpu_baseline(gc, b, mu, seconds):
     el = time.perf_counter() - t0
     out = {"value": iters / el, "unit": "iters/s", "cores": threads, "kind": "port",
            "sample": f"oracle/bpgl_oracle.c oracle_run, {iters} iterations from x=0 on the same "
-                     f"{H}x{gc.Block * W} fp32 A and b, {threads} OpenMP threads (fp64 arithmetic)"}
+                     f"{H}x{gc.Block * W} fp32 A and b{share_note}, {threads} OpenMP threads (fp64 arithmetic)",
+           "host": cpu_info}
     # SURVEY 8d also asks for the numpy restatement (OpenBLAS GEMVs, fp64) beside it: a few
     # iterations, bounded to about a third of the C sample's time
     A64 = A.astype(np.float64)
@@ -363,23 +486,22 @@ def main_panel(args):
     del Ab
     torch.cuda.synchronize()
 
-    def window(graph):
-        pl.solver_reset(B, mu, use_graph=graph)
-        pl.set_kernel_timing(not graph)
-        pl.solver_step(args.warmup)
+    def sync():
         pl.stream.synchronize()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        pl.solver_step(args.steps)
-        pl.stream.synchronize()
-        el = time.perf_counter() - t0
-        return el
 
-    el_graph = window(True)
-    st = pl.solver_status()
-    el_ev = window(False)
+    ctx = Ctx(1)
+    pl.solver_reset(B, mu, use_graph=True)
+    pl.solver_step(args.warmup)
+    sync()
+    n_ev = max(args.steps, 512)          # eager window: kernel averages + clock ramp
+    pl.set_kernel_timing(True)
+    el_ev = timed_window(ctx, sync, pl.solver_step, n_ev)
     kms, samples = pl.kernel_times()
     pl.set_kernel_timing(False)
+    wins = [timed_window(ctx, sync, pl.solver_step, args.steps) for _ in range(args.windows)]
+    st = pl.solver_status()
+    el_graph = median(wins)
     w = pl.MAT_WIDTH
     dom = max(("pass1_mfma", "pass2_mfma"), key=lambda q: kms[q])
     pb = panel_bytes_pass(m, w, k)
@@ -408,7 +530,10 @@ def main_panel(args):
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
             "iter_roofline_frac": iters_s * alg_iter / (HBM_PEAK_GBS * 1e9),
             "rhs_iters_per_s": iters_s * k,
-            "iters_per_s_eager_with_events": args.steps / el_ev,
+            "iters_per_s_eager_with_events": n_ev / el_ev,
+            "launch_mode": f"hipGraph replay, median of {args.windows} windows of {args.steps} iterations (value); "
+                           f"eager + HIP events over {n_ev} iterations (kernel times)",
+            "windows_s": wins,
             "kernel_avg_ms": kms, "status": st,
         },
         "roofline": {
@@ -420,6 +545,10 @@ def main_panel(args):
             "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)",
             "alg_bytes_per_launch": pb,
             "avg_launch_ms": kms[dom],
+            # whole iteration on the driver-visible clock: SURVEY 8d's bytes per iteration (the two
+            # MFMA passes over A + the panel vector I/O) / ms_per_step / peak
+            "iteration_frac_end_to_end": alg_iter / (el_graph / args.steps) / (HBM_PEAK_GBS * 1e9),
+            "survey_two_pass_frac": alg_iter / (el_graph / args.steps) / (HBM_PEAK_GBS * 1e9),
             "mfma": {"achieved_tflops": tflops, "peak_tflops": MFMA_BF16_DENSE_TFLOPS,
                      "frac": tflops / MFMA_BF16_DENSE_TFLOPS, "flops_per_launch": flops},
         },
@@ -448,6 +577,11 @@ def emit(out):
 def main():
     args = parse()
     quiet_stdout()
+    rank = int(os.environ.get("RANK", "0"))
+    cores, cpu_info = host_cores()
+    pool = None
+    if rank == 0 and not args.no_cpu and args.rhs == 1:
+        pool = cpu_pool_leg(cores)     # forks worker processes: before anything touches the GPU
     if args.rhs > 1:
         return main_panel(args)
     import torch
@@ -458,8 +592,12 @@ def main():
     res = measure(ctx, args, m, n_total)
     w, ml = res["w_local"], res["m_local"]
     rows = res["gc"].shard == "rows"
-    iters_s_graph = args.steps / res["el_graph"]
-    iters_s_ev = args.steps / res["el_events"]
+    K = args.steps
+    ok = [x for x in res["windows"] if not x["lost_iterations"]]
+    el_med = median([x["s_amortised"] for x in ok])
+    el_raw = median([x["s"] for x in ok])
+    iters_s = K / el_med
+    iters_s_ev = res["n_events"] / res["el_events"]
     kms = res["kernel_ms"]
     sa = {"float": 4, "double": 8, "bf16": 2}[args.type]
     onepass = kms.get("onepass", 0.0) > 0
@@ -468,56 +606,64 @@ def main():
         it_bytes = alg_bytes_iter_onepass(ml, w, sa)
     else:
         dom = max(("colpass", "rowpass"), key=lambda k: kms[k])
-        dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(m, w, sa)
+        dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(ml, w, sa)
         kname = {("colpass", 1): "k_iter_a", ("rowpass", 1): "k_iter_b",
                  ("colpass", 0): "k_colpass", ("rowpass", 0): "k_rowpass"}[(dom, int(args.fused))]
-        it_bytes = alg_bytes_iter(m, w, sa)
+        it_bytes = alg_bytes_iter(ml, w, sa)
+    two_pass_bytes = alg_bytes_iter(ml, w, sa)
     achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
     workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}" + ("_rows" if rows and G > 1 else "")
     traffic = pmc_traffic(workload_key, kname)
+    weak = G > 1 and not args.strong_total
+    ms_step = el_med / K * 1e3
+    allreduce_ms = ctx.gather(kms.get("allreduce", 0.0)) if G > 1 or args.comm else None
     out = {
         "metric": METRIC,
-        "value": iters_s_graph * G,
+        "value": iters_s * G if weak else iters_s,
         "unit": "block-iters/s (1 block-iter = one iteration's worth of an 8192x65536 fp32 matrix, "
-                "the per-GPU share; = N x global iterations/s)"
-        if G > 1 else "iters/s",
+                "the per-GPU share; = N x global iterations/s)" if weak else "iters/s",
         "n_gpus": G,
-        "steps": args.steps,
+        "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": res["el_graph"] / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong_total and G > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (A ~ N(0,1) rows unit-norm, generated in HBM; x_true density 0.4; b = A x_true + 0.01 e)",
         "config": {
-            "workload": ("configs[1]: m=8192 n=65536 fp32 A, 1 feature block, 1 GPU" if G == 1 else
-                         f"configs[2]-style: m={m} n={n_total} fp32 A, 1 feature block, row-sharded "
-                         f"{ml} rows/GPU x {G} GPUs, one RCCL all-reduce of n+2 fp64 per iteration" if rows else
-                         f"configs[2]-style: m={m} n={n_total} fp32 A, 1 feature block, column-sharded "
-                         f"{w} cols/GPU x {G} GPUs, RCCL all-reduce of m+2+N fp64 per iteration"),
+            "workload": workload_label(args, G, m, n_total, ml, w, rows),
             "m": m, "n": n_total, "m_local": ml, "n_local": w, "feature_blocks": args.block,
             "a_storage": args.type, "accumulate": "fp64",
-            "parallelism": f"{'row' if rows else 'column'}-shard x{G}", "rccl": bool(G > 1 or args.comm),
+            "parallelism": f"{'row' if rows else 'column'}-shard x{G}", "split": "rows" if rows else "columns",
+            "split_rule": "auto: rows for one feature block (one pass over A, DESIGN.md section 6 cost model), "
+                          "columns for several" if parse_shard_auto() else "--shard " + args.shard,
+            "rccl": bool(G > 1 or args.comm),
             "exchange": ("fp32 (U rounded, scalars hi+lo)" if rows and (G > 1 or args.comm) and args.exchange_fp32
                          else "fp64"),
-            "global_iters_per_s": iters_s_graph,
+            "global_iters_per_s": iters_s,
             "iteration": ("one pass over A (k_onepass: s23 = A D and U = A^T s23 together; g += gamma U, "
                           "exact g = A^T r every 256 iterations)" + (
-                              "; row shards: k_onepass_fold + RCCL all-reduce of [U | r.s23 | s23.s23]"
+                              "; row shards: k_onepass_fold + RCCL all-reduce of [U | r.s23 | s23.s23 | failed]"
                               if rows and G > 1 else "") if onepass else
                           "two passes over A (A^T r, then A D)"),
             "alg_bytes_per_iter_per_gpu": it_bytes,
             "hbm_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / it_bytes,
-            "iter_roofline_frac": iters_s_graph * it_bytes / (HBM_PEAK_GBS * 1e9),
-            "two_pass_alg_bytes_per_iter_per_gpu": alg_bytes_iter(ml, w, sa),
-            "two_pass_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / alg_bytes_iter(ml, w, sa),
-            # SURVEY 8d's iteration roofline (two passes over A): > 1 means the one-pass iteration
-            # beats what any two-pass implementation could reach at 8 TB/s
-            "two_pass_iter_roofline_frac": iters_s_graph * alg_bytes_iter(ml, w, sa) / (HBM_PEAK_GBS * 1e9),
-            "launch_mode": "hipGraph replay of one iteration (value); eager + HIP events (kernel times)", "fused": args.fused,
+            "iter_roofline_frac": iters_s * it_bytes / (HBM_PEAK_GBS * 1e9),
+            "two_pass_alg_bytes_per_iter_per_gpu": two_pass_bytes,
+            "two_pass_roofline_iters_per_s_per_gpu": HBM_PEAK_GBS * 1e9 / two_pass_bytes,
+            "launch_mode": (f"hipGraph replay, median of {len(ok)} windows of exactly {K} iterations (value); "
+                            f"eager + HIP events over {res['n_events']} iterations (kernel times)"),
+            "windows": res["windows"],
+            "ms_per_step_raw_median": el_raw / K * 1e3,
+            "refresh": {"period": res["refresh_period"], "ms_per_refresh": res["refresh_ms"],
+                        "folded": "window time - refreshes inside x ms_per_refresh + K/period x ms_per_refresh"},
+            "onepass_recoveries": {"fallbacks": res["fallbacks"], "retries": res["retries"]},
+            "fused": args.fused,
             "iters_per_s_eager_with_events": iters_s_ev,
             "kernel_avg_ms": kms,
+            "allreduce_ms_per_rank": allreduce_ms,
+            "status": res["status"],
         },
         "roofline": {
             "bound": "hbm",
@@ -531,27 +677,41 @@ def main():
             if traffic else None,
             "alg_bytes_per_launch": dom_bytes,
             "avg_launch_ms": kms[dom],
+            # the whole iteration on the driver-visible clock (ms_per_step, per GPU): the bytes this
+            # iteration must move / time / peak ...
+            "iteration_frac_end_to_end": it_bytes / (ms_step * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            # ... and SURVEY 8d's two-pass bytes (2 m w s_A + 8 (5w + 5m)) over the same time: > 1
+            # when one pass over A replaces two (8d's figure is superseded)
+            "survey_two_pass_frac": two_pass_bytes / (ms_step * 1e-3) / (HBM_PEAK_GBS * 1e9),
         },
     }
-    if G > 1 and not args.no_strong:
+    if ctx.rank == 0 and not args.no_cpu:
+        note = "" if G == 1 else f" (rank 0's share of the {G}-GPU problem: {ml} x {w})"
+        out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds, cores, cpu_info, note)
+        out["cpu_baseline"]["pool_configs0"] = pool
+    if G > 1 and not args.no_strong and not args.strong_total:
         del res
         torch.cuda.empty_cache()
         a2 = argparse.Namespace(**vars(args))
         strong = measure(ctx, a2, m, args.n_per_gpu)
-        out["strong"] = {"value": args.steps / strong["el_graph"], "unit": "iters/s",
+        so = [x for x in strong["windows"] if not x["lost_iterations"]]
+        out["strong"] = {"value": K / median([x["s_amortised"] for x in so]), "unit": "iters/s",
                          "config": f"m={m} n={args.n_per_gpu} split {G} ways ({strong['m_local']} rows x "
                                    f"{strong['w_local']} cols per GPU)",
-                         "kernel_avg_ms": strong["kernel_ms"]}
+                         "kernel_avg_ms": strong["kernel_ms"],
+                         "allreduce_ms_per_rank": ctx.gather(strong["kernel_ms"].get("allreduce", 0.0))}
         res = strong
     if G == 1 and args.type == "float":
         out["config"]["vendor_gemv_yardstick"] = vendor_yardstick(res["gc"])
         out["config"]["vendor_iteration_yardstick"] = vendor_iteration_yardstick(res["gc"], res["b"], res["mu"])
-    if G == 1 and ctx.rank == 0 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds)
     if ctx.rank == 0:
         emit(out)
     if ctx.world > 1:
         ctx.dist.destroy_process_group()
+
+
+def parse_shard_auto():
+    return "--shard" not in sys.argv
 
 
 if __name__ == "__main__":

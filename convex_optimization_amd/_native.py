@@ -59,6 +59,7 @@ _SIGS = {
     "bpgl_solver_step": (_int, [_p, _i64]),
     "bpgl_solver_status": (_int, [_p, ctypes.POINTER(_i64), ctypes.POINTER(_int), ctypes.POINTER(_i64),
                                   ctypes.POINTER(_f64), ctypes.POINTER(_f64)]),
+    "bpgl_solver_stat": (_int, [_p, ctypes.c_char_p, ctypes.POINTER(_i64)]),
     "bpgl_solver_residual": (_p, [_p]),
     "bpgl_iterate": (_int, [_p, _i64, _p, _f64, _p, _p, _p, _p, _f64, ctypes.POINTER(_i64)]),
     "bpgl_set_kernel_timing": (_int, [_p, _int]),

@@ -41,7 +41,7 @@ int fail(int code, const char* fmt, ...) {
 using namespace bpgl_host;
 
 namespace {
-constexpr int kTimedKinds = 8;
+constexpr int kTimedKinds = 9;   // + 8: the exact-gradient refresh of the one-pass iteration
 constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
@@ -70,7 +70,9 @@ struct bpgl_ctx {
     hipGraphExec_t gexec_k = nullptr;   // kGraphIters iterations (amortises the per-replay gap)
     // timing
     bool timing = false;
-    std::vector<hipEvent_t> evs;   // (kinds + 1) events per timed iteration
+    std::vector<hipEvent_t> evs;   // 2 events per (timed iteration, kind)
+    std::vector<hipEvent_t> ref_evs;   // 2 events per timed exact-gradient refresh (kind 8)
+    int64_t ref_timed = 0;
     int64_t timed_iters = 0;
     bool kind_used[kTimedKinds] = {};
     double wall_tick_s = 1e-8;
@@ -99,6 +101,12 @@ struct bpgl_ctx {
     int xch32 = 0;   // row shards' per-iteration exchange in fp32 ("exchange_fp32"; opt-in, -1 = RCCL only)
     bool op_refresh_pending = false;   // external rows: phase 2 ran, phase 3 not yet
     int64_t op_t = 0;          // iterations enqueued since the solver reset
+    int64_t req_t = 0;         // iterations requested since the solver reset (bpgl_solver_step)
+    int64_t op_fail_at = -1;   // test hook "onepass_fail_at": the launch of this iteration reports a failure
+    // counters since the solver reset (bpgl_solver_stat)
+    int64_t n_refresh = 0;     // exact-gradient refreshes enqueued
+    int64_t n_fallback = 0;    // one-rank one-pass solves moved to the two-pass kernels after a failure
+    int64_t n_retry = 0;       // row-shard one-pass iterations re-run after a failure
     OnePassArgs op{};
 };
 
@@ -163,8 +171,8 @@ Layout layout(const bpgl_ctx* c) {
     L.parts2 = k.take(8 * 2 * std::max<int64_t>(kMaxReduceBlocks, c->nchunk));
     L.Dbuf = k.take(8 * 2 * c->wp);
     L.cnt = k.take(8 * ((int64_t)c->nseg + c->nchunk));
-    // column shards exchange [s23 (m) | 2 | err slots]; row shards [U (wp) | r.s23 | s23.s23]
-    L.comm = k.take(8 * std::max<int64_t>(c->m + 2 + kMaxRanks, c->wp + 2));
+    // column shards exchange [s23 (m) | 2 | err slots]; row shards [U (wp) | r.s23 | s23.s23 | failed]
+    L.comm = k.take(8 * std::max<int64_t>(c->m + 2 + kMaxRanks, c->wp + 3));
     L.r = k.take(8 * c->m);
     L.Ax = k.take(8 * (int64_t)c->nblock * c->m);
     L.diag = k.take(8 * (int64_t)c->nblock * c->wp);
@@ -388,6 +396,7 @@ int onepass_local_gradient(bpgl_ctx* c, double* dst) {
 // exact g = A^T r into G (at reset and every op_refresh iterations); row shards sum it over ranks
 int onepass_refresh(bpgl_ctx* c) {
     int rc;
+    c->n_refresh++;
     if ((rc = onepass_local_gradient(c, c->op.G))) return rc;
     if (c->rows && c->comm && (rc = allreduce_sum(c, c->op.G, c->wp))) return rc;
     return onepass_tail<false>(c);   // the shrink of the next iteration from the exact g
@@ -411,10 +420,23 @@ int check_ready(const bpgl_ctx* c) {
     return 0;
 }
 
-// kinds: 0 colpass, 1 shrink, 2 rowpass, 3 rowreduce, 4 allreduce, 5 step, 6 update;
-// event 2 * (it * kinds + kind) + {0: start, 1: end}
+// kinds: 0 colpass, 1 shrink, 2 rowpass, 3 rowreduce, 4 allreduce, 5 step, 6 update, 7 onepass;
+// event 2 * (it * kinds + kind) + {0: start, 1: end}.  Kind 8 (the refresh, not in every
+// iteration) has its own event list, 2 per refresh.
 void ev_record(bpgl_ctx* c, int64_t it, int kind, int end) {
     if (!c->timing) return;
+    if (kind == 8) {
+        const size_t idx = 2 * (size_t)c->ref_timed + end;
+        while (c->ref_evs.size() <= idx) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            c->ref_evs.push_back(e);
+        }
+        (void)hipEventRecord(c->ref_evs[idx], c->stream);
+        if (end) c->ref_timed++;
+        c->kind_used[kind] = true;
+        return;
+    }
     const size_t idx = 2 * ((size_t)it * kTimedKinds + kind) + end;
     while (c->evs.size() <= idx) {
         hipEvent_t e;
@@ -474,13 +496,12 @@ int finalize_fused(bpgl_ctx* c) {
 // fold r.s23 and s23.s23, and the last group to finish runs the line search); phase 1:
 // k_onepass_tail (x, Ax, r, g += gamma U and the next iteration's shrink)
 //
-// Row shards: k_onepass, k_onepass_fold -> exchange buffer, all-reduce (RCCL), k_linesearch on
-// the summed scalars; phase 1: k_onepass_tail with the summed U.  With the exchange done by the
-// caller (external ranks) phase 0 ends after the fold and phase 1 starts with the line search.
+// Row shards: k_onepass, k_onepass_fold -> exchange buffer [U | r.s23 | s23.s23 | failed],
+// all-reduce (RCCL); phase 1: k_onepass_tail, which runs the line search on the summed scalars
+// at its head and then applies the summed U.  With the exchange done by the caller (external
+// ranks) phase 0 ends after the fold and phase 1 is the tail.
 int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
-    Params ls = op_params(c);
-    ls.parts2 = c->p.comm + c->wp;   // [r.s23, s23.s23] summed over ranks
     if (phase == 0) {
         ev_record(c, it, 7, 0);
         if ((rc = onepass_launch(c))) return rc;
@@ -494,9 +515,9 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
         if (c->comm) {
             ev_record(c, it, 4, 0);
             if (xf) {
-                ncclResult_t nr = ncclAllReduce(xf, xf, (size_t)(c->wp + 4), ncclFloat32, ncclSum, c->comm, c->stream);
+                ncclResult_t nr = ncclAllReduce(xf, xf, (size_t)(c->wp + 5), ncclFloat32, ncclSum, c->comm, c->stream);
                 if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
-            } else if ((rc = allreduce_sum(c, c->p.comm, c->wp + 2))) {
+            } else if ((rc = allreduce_sum(c, c->p.comm, c->wp + 3))) {
                 return rc;
             }
             ev_record(c, it, 4, 1);
@@ -504,7 +525,6 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
     }
     // the line search runs at the head of k_onepass_tail (o.abe: the fold pre-summed the shrink
     // partials; [r.s23, s23.s23] come from the exchange buffer)
-    (void)ls;
     if (phase == 1) {
         ev_record(c, it, 6, 0);
         if ((rc = onepass_tail<true>(c))) return rc;
@@ -581,6 +601,102 @@ int enqueue_iteration(bpgl_ctx* c, int64_t it) {
     return enqueue_phase(c, it, 1);
 }
 
+// hipGraphs of 1 and kGraphIters iterations (c->use_graph), uploaded to the device here so the
+// first replay inside a caller's timed region pays no upload
+int capture_graphs(bpgl_ctx* c) {
+    drop_graphs(c);
+    if (!c->use_graph) return 0;
+    int rc = 0;
+    const bool was_timing = c->timing;
+    c->timing = false;
+    for (int variant = 0; variant < 2 && !rc; ++variant) {
+        const int iters = variant == 0 ? 1 : kGraphIters;
+        hipGraph_t graph = nullptr;
+        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        for (int k = 0; k < iters && !rc; ++k) rc = enqueue_iteration(c, 0);
+        hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+        if (rc) { if (graph) (void)hipGraphDestroy(graph); break; }
+        if (ec != hipSuccess) { rc = fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec)); break; }
+        hipGraphExec_t* dst = variant == 0 ? &c->gexec : &c->gexec_k;
+        hipError_t ei = hipGraphInstantiate(dst, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) { rc = fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei)); break; }
+        if ((ei = hipGraphUpload(*dst, c->stream)) != hipSuccess)
+            rc = fail(BPGL_E_HIP, "hipGraphUpload: %s", hipGetErrorString(ei));
+    }
+    c->timing = was_timing;
+    return rc;
+}
+
+// enqueue n_iter iterations (graph replays when captured), with the one-pass exact-gradient
+// refresh every op_refresh iterations
+int step_impl(bpgl_ctx* c, int64_t n_iter) {
+    int rc;
+    const int64_t K = c->op_on ? c->op_refresh : 0;
+    for (int64_t i = 0; i < n_iter;) {
+        if (K > 0 && c->op_t > 0 && c->op_t % K == 0) {
+            ev_record(c, c->timed_iters, 8, 0);
+            if ((rc = onepass_refresh(c))) return rc;
+            ev_record(c, c->timed_iters, 8, 1);
+        }
+        const int64_t room = K > 0 ? std::min<int64_t>(n_iter - i, K - c->op_t % K) : n_iter - i;
+        int64_t k = 1;
+        if (!c->timing && c->gexec_k && room >= kGraphIters) {
+            HIP_TRY(hipGraphLaunch(c->gexec_k, c->stream));
+            k = kGraphIters;
+        } else if (c->timing || !c->gexec) {
+            if ((rc = enqueue_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
+            if (c->timing) c->timed_iters++;
+        } else {
+            HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
+        }
+        i += k;
+        c->op_t += k;
+    }
+    return finalize_fused(c);
+}
+
+// A one-pass launch whose row hand-off ran out of polls (its blocks were not all resident:
+// another kernel or process held CUs) commits nothing, and neither does any iteration after
+// it until the flag is cleared (bpgl_onepass.h).  Re-run the iterations that were lost: one
+// rank moves to the two-pass kernels for the rest of this solve (they need no co-residency);
+// row shards run the lost iterations again on the one-pass kernels (every rank sees the same
+// summed failure flag, so every rank re-runs the same iterations; RCCL ranks must all call
+// bpgl_solver_status at the same point), at most kOpRetries times.
+constexpr int kOpRetries = 3;
+int read_state(bpgl_ctx* c, DevState& st) {
+    HIP_TRY(hipMemcpyAsync(&st, c->p.st, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+int recover_onepass(bpgl_ctx* c, DevState& st) {
+    int rc;
+    for (int attempt = 0; st.op_fail; ++attempt) {
+        HIP_TRY(hipMemsetAsync(&c->p.st->op_fail, 0, sizeof st.op_fail, c->stream));
+        const int64_t t = st.t;
+        c->op_fail_at = -1;   // the test hook fires once
+        c->op.fail_at = -1;
+        if (c->external)
+            return fail(BPGL_E_EXCHANGE, "one-pass row hand-off timed out (blocks not co-resident); iterations from "
+                                         "t = %lld on were not applied and the solver state is intact: run them again",
+                        (long long)t);
+        if (c->rows && attempt >= kOpRetries)
+            return fail(BPGL_E_EXCHANGE, "one-pass row hand-off timed out %d times in a row at t = %lld (another "
+                                         "kernel keeps CUs busy); the solver state is intact at t", kOpRetries + 1,
+                        (long long)t);
+        if (c->rows) {
+            c->n_retry += c->req_t - t;
+        } else {
+            c->op_on = false;
+            c->n_fallback++;
+        }
+        if ((rc = capture_graphs(c))) return rc;
+        if (!st.done && c->req_t > t && (rc = step_impl(c, c->req_t - t))) return rc;
+        if ((rc = read_state(c, st))) return rc;
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -635,6 +751,7 @@ void bpgl_destroy(bpgl_ctx* c) {
     (void)hipSetDevice(c->device);   // destroy path: nothing to report to
     drop_graphs(c);
     for (auto e : c->evs) (void)hipEventDestroy(e);
+    for (auto e : c->ref_evs) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -722,6 +839,7 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
         c->op.abe = c->rows ? (double*)(s + L.opABE) : nullptr;
         c->op.cache_permille = c->op_cache;
     }
+    c->op.fail_at = c->op_fail_at;
     HIP_TRY(hipSetDevice(c->device));
     if (c->op_shape) HIP_TRY(hipMemsetAsync(s + L.opPG, 0, 8 * c->m * c->op_SB, c->stream));   // tag 0: never written
     HIP_TRY(hipMemsetAsync(s + L.st, 0, sizeof(DevState), c->stream));
@@ -870,7 +988,7 @@ int bpgl_solver_phase(bpgl_ctx* c, int phase) {
             return fail(BPGL_E_STATE, "phases 2 and 3 exist for external row shards only");
         if (phase == 2) {
             if ((rc = onepass_local_gradient(c, c->p.comm))) return rc;
-            HIP_TRY(hipMemsetAsync(c->p.comm + c->wp, 0, 16, c->stream));
+            HIP_TRY(hipMemsetAsync(c->p.comm + c->wp, 0, 24, c->stream));
             c->op_refresh_pending = true;
             return 0;
         }
@@ -886,7 +1004,7 @@ int bpgl_solver_phase(bpgl_ctx* c, int phase) {
 
 double* bpgl_solver_exchange_buffer(bpgl_ctx* c, int64_t* count) {
     if (!c) return nullptr;
-    if (count) *count = c->rows ? c->wp + 2 : c->m + 2 + c->nranks;
+    if (count) *count = c->rows ? c->wp + 3 : c->m + 2 + c->nranks;
     return c->p.comm;
 }
 
@@ -934,26 +1052,10 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
         // external row shards: the caller runs the first exact gradient (phases 2 and 3)
         if (c->op_on && !(c->rows && c->external) && (rc = onepass_refresh(c))) return rc;
     }
-    drop_graphs(c);
     c->use_graph = use_graph != 0 && !c->external;
-    if (c->use_graph) {
-        const bool was_timing = c->timing;
-        c->timing = false;
-        for (int variant = 0; variant < 2; ++variant) {
-            const int iters = variant == 0 ? 1 : kGraphIters;
-            hipGraph_t graph = nullptr;
-            HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-            rc = 0;
-            for (int k = 0; k < iters && !rc; ++k) rc = enqueue_iteration(c, 0);
-            hipError_t ec = hipStreamEndCapture(c->stream, &graph);
-            if (rc) { if (graph) (void)hipGraphDestroy(graph); c->timing = was_timing; return rc; }
-            if (ec != hipSuccess) { c->timing = was_timing; return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec)); }
-            hipError_t ei = hipGraphInstantiate(variant == 0 ? &c->gexec : &c->gexec_k, graph, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(graph);
-            if (ei != hipSuccess) { c->timing = was_timing; return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei)); }
-        }
-        c->timing = was_timing;
-    }
+    if ((rc = capture_graphs(c))) return rc;
+    c->req_t = 0;
+    c->n_refresh = c->n_fallback = c->n_retry = 0;
     c->solver = true;
     c->timed_iters = 0;
     return 0;
@@ -966,24 +1068,8 @@ int bpgl_solver_step(bpgl_ctx* c, int64_t n_iter) {
     if (n_iter < 0) return fail(BPGL_E_ARG, "n_iter < 0");
     if (c->external) return fail(BPGL_E_STATE, "external-exchange ranks advance with bpgl_solver_phase");
     HIP_TRY(hipSetDevice(c->device));
-    const int64_t K = c->op_on ? c->op_refresh : 0;
-    for (int64_t i = 0; i < n_iter;) {
-        if (K > 0 && c->op_t > 0 && c->op_t % K == 0 && (rc = onepass_refresh(c))) return rc;
-        const int64_t room = K > 0 ? std::min<int64_t>(n_iter - i, K - c->op_t % K) : n_iter - i;
-        int64_t k = 1;
-        if (!c->timing && c->gexec_k && room >= kGraphIters) {
-            HIP_TRY(hipGraphLaunch(c->gexec_k, c->stream));
-            k = kGraphIters;
-        } else if (c->timing || !c->gexec) {
-            if ((rc = enqueue_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
-            if (c->timing) c->timed_iters++;
-        } else {
-            HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
-        }
-        i += k;
-        c->op_t += k;
-    }
-    return finalize_fused(c);
+    c->req_t += n_iter;
+    return step_impl(c, n_iter);
 }
 
 int bpgl_solver_status(bpgl_ctx* c, int64_t* iters_done, int* stopped, int64_t* t_last, double* gamma,
@@ -992,16 +1078,26 @@ int bpgl_solver_status(bpgl_ctx* c, int64_t* iters_done, int* stopped, int64_t* 
     if ((rc = check_ready(c))) return rc;
     HIP_TRY(hipSetDevice(c->device));
     DevState st;
-    HIP_TRY(hipMemcpyAsync(&st, c->p.st, sizeof st, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((rc = read_state(c, st))) return rc;
+    if (st.op_fail && c->solver && (rc = recover_onepass(c, st))) return rc;
     if (iters_done) *iters_done = st.iters;
     if (stopped) *stopped = (int)st.done;
     if (t_last) *t_last = st.t_last;
     if (gamma) *gamma = st.gamma;
     if (err) *err = st.err;
-    if (st.op_fail)
-        return fail(BPGL_E_EXCHANGE, "one-pass row hand-off timed out (another kernel held CUs while k_onepass "
-                                     "ran); reset the solver");
+    return 0;
+}
+
+int bpgl_solver_stat(bpgl_ctx* c, const char* key, int64_t* value) {
+    if (!c || !key || !value) return fail(BPGL_E_ARG, "null argument");
+    if (!strcmp(key, "onepass")) *value = c->op_on ? 1 : 0;
+    else if (!strcmp(key, "refresh_period")) *value = c->op_on ? c->op_refresh : 0;
+    else if (!strcmp(key, "refreshes")) *value = c->n_refresh;
+    else if (!strcmp(key, "fallbacks")) *value = c->n_fallback;
+    else if (!strcmp(key, "retries")) *value = c->n_retry;
+    else if (!strcmp(key, "requested")) *value = c->req_t;
+    else if (!strcmp(key, "enqueued")) *value = c->op_t;
+    else return fail(BPGL_E_ARG, "unknown stat '%s'", key);
     return 0;
 }
 
@@ -1077,6 +1173,13 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->solver = false;
         return 0;
     }
+    if (!strcmp(key, "onepass_fail_at")) {   // test hook: the one-pass launch of iteration `value` fails once
+        c->op_fail_at = value < 0 ? -1 : value;
+        c->op.fail_at = c->op_fail_at;
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
     if (!strcmp(key, "onepass_refresh")) {
         if (value < 0) return fail(BPGL_E_ARG, "onepass_refresh must be >= 0");
         c->op_refresh = (int)std::min<int64_t>(value, 1 << 30);
@@ -1095,6 +1198,7 @@ int bpgl_set_kernel_timing(bpgl_ctx* c, int enable) {
     if (!c) return fail(BPGL_E_ARG, "null context");
     c->timing = enable != 0;
     c->timed_iters = 0;
+    c->ref_timed = 0;
     for (int k = 0; k < kTimedKinds; ++k) c->kind_used[k] = false;
     return 0;
 }
@@ -1104,8 +1208,13 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     double sum[kTimedKinds] = {0};
+    for (int64_t r = 0; r < c->ref_timed; ++r) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ref_evs[2 * r], c->ref_evs[2 * r + 1]));
+        sum[8] += ms;
+    }
     for (int64_t it = 0; it < c->timed_iters; ++it) {
-        for (int k = 0; k < kTimedKinds; ++k) {
+        for (int k = 0; k < kTimedKinds - 1; ++k) {
             if (!c->kind_used[k]) continue;
             float ms = 0.f;
             const size_t i0 = 2 * ((size_t)it * kTimedKinds + k);
@@ -1117,6 +1226,7 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     for (int k = 0; k < kTimedKinds; ++k) avg_ms[k] = c->timed_iters ? sum[k] / c->timed_iters : 0.0;
     if (samples) *samples = c->timed_iters;
     c->timed_iters = 0;
+    c->ref_timed = 0;
     for (int k = 0; k < kTimedKinds; ++k) c->kind_used[k] = false;
     return 0;
 }

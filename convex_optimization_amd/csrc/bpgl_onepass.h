@@ -24,7 +24,13 @@
 //     them in one fixed order -> s23[t], bit-identical in every block; U += row * s23[t]
 //     (SB <= 64: one granule per lane; SB <= 128: lanes l and l + 64, GPL = 2);
 //   * a late granule is re-polled (bounded; on exhaustion the state's op_fail word is set
-//     and the kernel still finishes -- bpgl_solver_status reports BPGL_E_EXCHANGE).
+//     and the kernel still finishes).  A failed launch commits nothing: every block arrives
+//     at the line-search counter after setting op_fail, so the last arrival sees every
+//     failure of the launch and skips the line search (the iteration index does not
+//     advance), and k_onepass_tail skips the update while op_fail is set.
+//     bpgl_solver_status then re-runs the lost iterations (one rank: on the two-pass
+//     kernels for the rest of the solve; row shards: the same iteration again, with the
+//     failure flag summed over ranks so every rank skips the same iterations).
 // Outputs: s23 (by segment block 0) and one U partial row per row group; k_onepass_tail
 // folds the partials in a fixed order into g += gamma U after the line search.
 //
@@ -58,6 +64,7 @@ struct OnePassArgs {
     int cache_permille;          // share of each group's rows read last with cache-allocating loads
     const float* Uf;             // row shards, fp32 exchange: the all-reduced U (read instead of Us)
     double* abe;                 // row shards: [sum|Bx|, sum|x|, max err] of the last shrink (k_onepass_fold)
+    long long fail_at;           // test hook: iteration whose launch reports a hand-off failure (-1: none)
 };
 
 typedef unsigned long long op_u64;
@@ -123,7 +130,12 @@ __device__ __forceinline__ double op_quad_sum(double x) {
 // The line search of a one-rank one-pass iteration (lasso.py:129-150), run by the last row
 // group of k_onepass to finish: its r.s23 / s23.s23 partials (parts2, written through to
 // memory by every group) and the shrink partials of the previous k_onepass_tail, folded in
-// a fixed order.  The arrival counter only grows: launch k ends at count k * ngroups.
+// a fixed order.  Every block of the grid arrives (after publishing its failure, if any), so
+// the counter only grows and launch k ends at count k * gridDim.x.
+__device__ __forceinline__ bool op_failed(const Params& p) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&p.st->op_fail), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
 __device__ __forceinline__ bool op_arrive_last(unsigned long long* cnt, unsigned long long expected) {
     __shared__ int last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -151,7 +163,8 @@ __device__ void op_linesearch(const Params& p, int ngroups) {
     ss = ((sq[0] + sq[1]) + sq[2]) + sq[3];
     double a, b, e;
     fold_parts(p, p.nparts, a, b, e);
-    if (threadIdx.x == 0) finish_step(p, rs, ss, a, b, e);
+    // every block set op_fail (if it failed) before it arrived: a failed launch commits nothing
+    if (threadIdx.x == 0 && !op_failed(p)) finish_step(p, rs, ss, a, b, e);
 }
 
 template <int LU, typename T>
@@ -188,8 +201,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
     if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
         if (sb == 0 && threadIdx.x == 0) { st_sc1(p.parts2 + 2ll * grp, 0.0); st_sc1(p.parts2 + 2ll * grp + 1, 0.0); }
-        if (o.ls && sb == 0 && op_arrive_last(&p.st->op_cnt, (unsigned long long)o.ngroups))
-            op_linesearch(p, o.ngroups);
+        if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) op_linesearch(p, o.ngroups);
         return;
     }
     const unsigned tag = (unsigned)((p.st->op_epoch + 1) & 1);   // bound scratch is zero: parity 0 = unwritten
@@ -222,7 +234,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     raw buf[NB][LU];
     op_u64 gv[NB][GPL];
     unsigned polls = kOpPolls;
-    bool failed = false;
+    bool failed = o.fail_at >= 0 && b == 0 && p.st->t == o.fail_at;   // test hook (bpgl_set_tuning)
 
     const int tcache = nrows - (int)(((long long)nrows * o.cache_permille) / 1000);
     // NTL: the load policy, a compile-time choice per copy of the row loop (a runtime branch
@@ -359,15 +371,19 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         if (colok[k])
 #pragma unroll
             for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
-    if (o.ls && sb == 0 && op_arrive_last(&p.st->op_cnt, (unsigned long long)o.ngroups))   // block-uniform
+    if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x))   // block-uniform
         op_linesearch(p, o.ngroups);
 }
 
-// Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23]
-// (fixed order over the row groups).  Runs whether or not the solver stopped: the all-reduce
-// after it runs in every iteration of a captured graph.  `outf` (RCCL row shards, the
-// "exchange_fp32" knob): the same contribution as fp32 -- U rounded, each scalar as a hi + lo
-// pair [U (wp) | rs_hi | rs_lo | ss_hi | ss_lo] -- half the bytes on xGMI.
+// Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23 |
+// failed] (fixed order over the row groups; `failed` = this rank's op_fail, so the sum tells
+// every rank whether any rank's launch failed).  Runs whether or not the solver stopped: the
+// all-reduce after it runs in every iteration of a captured graph.  `outf` (RCCL row shards,
+// the "exchange_fp32" knob): the same contribution as fp32 -- U rounded, each scalar split
+// into a hi + lo pair [U (wp) | rs_hi | rs_lo | ss_hi | ss_lo | failed] -- half the bytes on
+// xGMI.  With one rank the pair carries the scalar to ~2^-48; RCCL sums the hi words and the
+// lo words separately in fp32, so with several ranks each summed word is rounded to fp32 and
+// the scalars are only fp32-accurate (~2^-24 relative).
 __device__ __forceinline__ void op_split_f32(double v, float* dst) {
     const float hi = (float)v;
     dst[0] = hi;
@@ -393,12 +409,15 @@ __global__ __launch_bounds__(kThreads) void k_onepass_fold(Params p, OnePassArgs
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         double rs = 0.0, ss = 0.0;
         for (int q = 0; q < o.ngroups; ++q) { rs += p.parts2[2ll * q]; ss += p.parts2[2ll * q + 1]; }
+        const bool failed = op_failed(p);
         if (outf) {
             op_split_f32(rs, outf + p.wp);
             op_split_f32(ss, outf + p.wp + 2);
+            outf[p.wp + 4] = failed ? 1.0f : 0.0f;
         } else {
             out[p.wp] = rs;
             out[p.wp + 1] = ss;
+            out[p.wp + 2] = failed ? 1.0 : 0.0;
         }
     }
 }
@@ -419,12 +438,26 @@ __global__ __launch_bounds__(kThreads) void k_recip(const double* __restrict__ d
 // (it runs in the iteration whose line search stops, too).
 template <bool UPDATE>
 __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs o) {
+    // the parity advances after every k_onepass launch, a failed one too (it still published
+    // every granule of its rows)
     if (UPDATE && blockIdx.x == 0 && threadIdx.x == 0 && p.st->op_ran) {
         p.st->op_epoch += 1;
         p.st->op_ran = 0;
     }
     if (p.st->done) return;
+    // a failed k_onepass (this iteration or an earlier one not yet re-run) commits nothing
+    if (UPDATE && op_failed(p)) return;
     double gamma = UPDATE ? p.st->gamma : 0.0;
+    if (UPDATE && o.abe) {
+        // row shards: any rank's failure, summed over ranks -> every rank skips this iteration
+        const double failed = o.Uf ? (double)o.Uf[p.wp + 4] : o.Us[p.wp + 2];
+        if (failed != 0.0) {   // grid-uniform
+            if (blockIdx.x == 0 && threadIdx.x == 0)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(&p.st->op_fail), 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
     if (UPDATE && o.abe) {
         // row shards: the line search (lasso.py:129-150) on the all-reduced [r.s23, s23.s23] and the
         // fold's shrink sums, computed identically by every block (the same inputs, the same

@@ -343,6 +343,9 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
         hipError_t ei = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+        // uploaded here, so the first replay in a caller's timed region pays no upload
+        if ((ei = hipGraphUpload(c->gexec, c->stream)) != hipSuccess)
+            return fail(BPGL_E_HIP, "hipGraphUpload: %s", hipGetErrorString(ei));
     }
     c->solver = true;
     c->timed_iters = 0;

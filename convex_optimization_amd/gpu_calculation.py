@@ -265,6 +265,13 @@ class GPU_Calculation:
                                            ctypes.byref(ga), ctypes.byref(er)), "bpgl_solver_status")
         return dict(iters=it.value, stopped=bool(st.value), t_last=tl.value, gamma=ga.value, err=er.value)
 
+    def solver_stat(self, key):
+        """Counter since the last reset (include/bpgl.h bpgl_solver_stat): "onepass", "refreshes",
+        "fallbacks", "retries", "requested", "enqueued"."""
+        v = ctypes.c_int64()
+        N.check(N.lib().bpgl_solver_stat(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_solver_stat")
+        return v.value
+
     def solver_x(self):
         """Current iterate as a host ndarray (K_local,) in the reference's block order."""
         self.stream.synchronize()
@@ -302,9 +309,10 @@ class GPU_Calculation:
 
     def exchange_buffer(self, fp32=False):
         """Device view of the per-iteration exchange (lives in the scratch): column shards
-        [s23 (m) | sum|Bx| | sum|x| | err slot per rank]; row shards [U (w_pad) | r.s23 | s23.s23].
-        ``fp32``: the row shards' fp32 format of phases 0/1 ("exchange_fp32" = 1), w_pad + 4
-        float32 [U | r.s23 hi, lo | s23.s23 hi, lo] at the same address."""
+        [s23 (m) | sum|Bx| | sum|x| | err slot per rank]; row shards [U (w_pad) | r.s23 | s23.s23 |
+        failed] (``failed``: the rank's one-pass failure flag, see include/bpgl.h).
+        ``fp32``: the row shards' fp32 format of phases 0/1 ("exchange_fp32" = 1), w_pad + 5
+        float32 [U | r.s23 hi, lo | s23.s23 hi, lo | failed] at the same address."""
         cnt = ctypes.c_int64()
         addr = N.lib().bpgl_solver_exchange_buffer(self._ctx, ctypes.byref(cnt))
         off = (addr - self._scratch.data_ptr()) // 8
@@ -318,7 +326,8 @@ class GPU_Calculation:
     def set_kernel_timing(self, enable):
         N.check(N.lib().bpgl_set_kernel_timing(self._ctx, int(bool(enable))), "bpgl_set_kernel_timing")
 
-    KERNEL_KINDS = ("colpass", "shrink", "rowpass", "rowreduce", "allreduce", "step", "update", "onepass")
+    KERNEL_KINDS = ("colpass", "shrink", "rowpass", "rowreduce", "allreduce", "step", "update", "onepass",
+                    "refresh")
 
     def kernel_times(self):
         arr = (ctypes.c_double * len(self.KERNEL_KINDS))()

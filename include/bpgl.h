@@ -41,8 +41,11 @@ enum {
     BPGL_E_RCCL = -4,     /* RCCL error                                  */
     BPGL_E_SCRATCH = -5,  /* scratch buffer too small                    */
     BPGL_E_EXCHANGE = -6  /* one-pass row hand-off timed out (another
-                             kernel held CUs); the solver state is
-                             invalid until the next bpgl_solver_reset     */
+                             kernel held CUs) and could not be recovered
+                             (external-exchange ranks, or row shards that
+                             failed kOpRetries + 1 times in a row); the
+                             failed iterations committed nothing: the
+                             solver state is intact at the reported t     */
 };
 
 typedef struct bpgl_ctx bpgl_ctx;
@@ -126,8 +129,9 @@ int bpgl_comm_init(bpgl_ctx* ctx, const void* unique_id128, int rank, int nranks
  * q holds rows [m_q, m_{q+1}) of A (the context's m is its row count, n_local the
  * full width), b and the residual are local, x is replicated.  Row shards run the
  * one-pass iteration (A read once per iteration): per iteration one all-reduce
- * (SUM) of [A^T A D | r.s23 | s23.s23] -- w_pad + 2 fp64, or (opt-in tuning key
- * "exchange_fp32") w_pad + 4 fp32 (U rounded, the scalars as hi + lo pairs);
+ * (SUM) of [A^T A D | r.s23 | s23.s23 | failed] -- w_pad + 3 fp64, or (opt-in
+ * tuning key "exchange_fp32") w_pad + 5 fp32 (U rounded, the scalars as hi + lo
+ * pairs; fp32-accurate once summed over several ranks);
  * bpgl_diag_ata and every
  * exact gradient refresh all-reduce w_pad values.  There is no reference
  * counterpart: the reference shards columns only (cpu_calculation.py:23-27).
@@ -144,13 +148,15 @@ int bpgl_set_shard(bpgl_ctx* ctx, int mode);
  * writes the sum back on every rank; bpgl_solver_phase(ctx, 1).  Requires the
  * initial point x = 0.
  */
-/* Row shards (count = w_pad + 2): the same two phases per iteration; in
+/* Row shards (count = w_pad + 3): the same two phases per iteration; in
  * addition the exact gradient g = A^T r is exchanged by phase 2 (this rank's
  * A_q^T r_q into the exchange buffer), the caller's sum, and phase 3 -- after
  * bpgl_solver_reset and again every "onepass_refresh" iterations.  With the
- * tuning key "exchange_fp32" = 1 phases 0/1 exchange w_pad + 4 fp32 at the same
- * address instead: [U (w_pad) | r.s23 hi, lo | s23.s23 hi, lo]; phases 2/3 stay
- * fp64. */
+ * tuning key "exchange_fp32" = 1 phases 0/1 exchange w_pad + 5 fp32 at the same
+ * address instead: [U (w_pad) | r.s23 hi, lo | s23.s23 hi, lo | failed]; phases
+ * 2/3 stay fp64.  The `failed` slot is each rank's one-pass failure flag: a
+ * nonzero sum makes every rank skip the iteration (bpgl_solver_status then
+ * reports BPGL_E_EXCHANGE with the state intact, and the caller re-runs it). */
 int bpgl_set_ranks(bpgl_ctx* ctx, int rank, int nranks);
 int bpgl_solver_phase(bpgl_ctx* ctx, int phase);
 double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
@@ -168,7 +174,17 @@ double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
  * bpgl_solver_step: enqueue n_iter more iterations (asynchronous; replays a
  *   captured hipGraph of one iteration when `use_graph` was set).
  * bpgl_solver_status: synchronise the stream and read (iterations done,
- *   stopped flag, last t, last step size, last error).
+ *   stopped flag, last t, last step size, last error).  It also completes
+ *   iterations a one-pass launch lost: a launch whose blocks were not all
+ *   resident (another kernel or process held CUs) commits nothing, nor does
+ *   any later iteration until this call re-runs them -- one rank on the
+ *   two-pass kernels for the rest of the solve, row shards on the one-pass
+ *   kernels again (RCCL row-shard ranks must all call it at the same point).
+ * bpgl_solver_stat: counters since the last reset -- "onepass" (1 while the
+ *   one-pass iteration is in use), "refresh_period" (iterations between
+ *   exact-gradient refreshes, 0 = none), "refreshes" (exact-gradient refreshes
+ *   enqueued), "fallbacks" / "retries" (recoveries above), "requested"
+ *   (iterations asked of bpgl_solver_step), "enqueued".
  * bpgl_solver_residual: device pointer of the residual s11 = sum_k Ax_k - b (m).
  */
 int bpgl_solver_reset(bpgl_ctx* ctx, const double* b, double mu, double* x,
@@ -178,6 +194,7 @@ int bpgl_solver_reset(bpgl_ctx* ctx, const double* b, double mu, double* x,
 int bpgl_solver_step(bpgl_ctx* ctx, int64_t n_iter);
 int bpgl_solver_status(bpgl_ctx* ctx, int64_t* iters_done, int* stopped, int64_t* t_last,
                        double* gamma, double* err);
+int bpgl_solver_stat(bpgl_ctx* ctx, const char* key, int64_t* value);
 const double* bpgl_solver_residual(bpgl_ctx* ctx);
 
 /*
@@ -194,10 +211,11 @@ int bpgl_iterate(bpgl_ctx* ctx, int64_t n_iter, const int32_t* order, double mu,
  * kinds: 0 colpass (A^T r), 1 shrink, 2 rowpass (A D), 3 rowreduce (+ line
  * search on one rank), 4 allreduce, 5 step (multi-rank line search), 6 update
  * (+ gradient update in one-pass mode), 7 onepass (A D and A^T (A D) in one
- * pass over A).  Row shards: 3 = fold of the exchange contribution, 5 = line
- * search. */
+ * pass over A), 8 refresh (the one-pass exact-gradient refresh, amortised:
+ * its total time over the window's iterations).  Row shards: 3 = fold of the
+ * exchange contribution (the line search runs in 6). */
 int bpgl_set_kernel_timing(bpgl_ctx* ctx, int enable);
-int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
+int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
 
 /* Runtime tuning knobs (call before bpgl_solver_reset).  These do not change
  * results:
@@ -223,6 +241,8 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 8 */, int64_t* samples);
  *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for
  *   a caller-side exchange): row shards' per-iteration exchange in fp32 -- half the
  *   bytes, x within 2e-7 (1 rank) to 1.5e-6 (8 ranks) of the fp64 exchange.
+ *   "onepass_fail_at" (test hook, default -1): the one-pass launch of iteration t
+ *   reports a row hand-off failure once (exercises the recovery above).
  * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the
  * number of (row chunk x column segment) tiles per two-pass launch (default
  * 1024 for fp32 A, 512 for fp64 / bf16). */

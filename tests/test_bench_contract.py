@@ -84,3 +84,58 @@ def test_emit_writes_one_json_line():
     b.emit({"metric": "m", "value": 1.0})
     lines = buf.getvalue().splitlines()
     assert len(lines) == 1 and json.loads(lines[0])["value"] == 1.0
+
+
+def _parse(b, argv):
+    import sys
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py"] + argv
+        return b.parse()
+    finally:
+        sys.argv = old
+
+
+def test_config_mapping_and_split_rule():
+    """--config 2 is configs[2]'s own problem (8192 x 524288) split over the GPUs (strong);
+    --shard auto picks rows for one feature block and columns for several"""
+    b = _bench()
+    a = _parse(b, ["--config", "2", "--gpus", "8"])
+    assert (a.m, a.n_per_gpu, a.strong_total, a.shard) == (8192, 65536, True, "rows")
+    a = _parse(b, ["--config", "2"])
+    assert (a.m, a.n_per_gpu) == (8192, 524288)
+    assert _parse(b, ["--block", "2"]).shard == "columns"
+    assert _parse(b, ["--block", "2", "--shard", "rows"]).shard == "rows"
+    a = _parse(b, ["--config", "3"])
+    assert (a.m, a.n_per_gpu) == (1048576, 4096)
+
+
+def test_workload_labels_follow_the_shape():
+    b = _bench()
+    a = _parse(b, ["--config", "3"])
+    assert b.workload_label(a, 1, 1048576, 4096, 1048576, 4096, False).startswith("configs[3]:")
+    a = _parse(b, [])
+    assert b.workload_label(a, 1, 8192, 65536, 8192, 65536, False).startswith("configs[1]:")
+    assert "row-sharded 1024 rows/GPU" in b.workload_label(a, 8, 8192, 524288, 1024, 524288, True)
+    a = _parse(b, ["--config", "2", "--gpus", "8"])
+    assert b.workload_label(a, 8, 8192, 524288, 1024, 524288, True).startswith("configs[2]:")
+
+
+def test_host_cores_and_window_median():
+    b = _bench()
+    n, info = b.host_cores()
+    assert 1 <= n <= (os.cpu_count() or 1) and info["affinity"] >= 1 and info["threads"] == n
+    assert b.median([3.0, 1.0, 2.0]) == 2.0 and b.median([4.0, 1.0, 2.0, 3.0]) == 2.5
+
+
+def test_pool_baseline_matches_oracle():
+    """the Pool-parallel CPU leg (the reference's ClassLassoCPU structure, oracle/pool_baseline.py)
+    computes the reference iteration: same x as the C oracle with the same P-way split"""
+    import numpy as np
+    from oracle import oracle
+    from oracle.pool_baseline import instance, largest_divisor_at_most, run_pool
+    A, bb, mu = instance(128, 512, seed=3)
+    x, el, _ = run_pool(A, bb, mu, 2, 4, 12)
+    ref = oracle.run(A, bb, mu, 2, 12, P=4)["x"]
+    assert np.linalg.norm(x - ref) <= 1e-10 * np.linalg.norm(ref)
+    assert largest_divisor_at_most(2048, 12) == 8 and largest_divisor_at_most(2048, 64) == 64

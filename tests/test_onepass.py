@@ -169,3 +169,78 @@ def test_full_size_matches_oracle():
     ref = oracle.run(np.ascontiguousarray(A_host), b.cpu().numpy(), mu, 1, 8, nthreads=16)
     assert rel(res["x"], ref["x"]) <= 1e-5
     assert rel(res["x"], ref["x"]) <= 1e-10, rel(res["x"], ref["x"])
+
+
+@pytest.mark.parametrize("fail_at,use_graph", [(37, True), (0, False), (199, True)])
+def test_hand_off_failure_falls_back_to_two_pass(golden, fail_at, use_graph):
+    """A k_onepass launch whose row hand-off runs out of polls (its blocks were not all resident:
+    another kernel or process held CUs) commits nothing -- the last block to arrive sees the
+    failure and skips the line search, the tail skips the update -- and neither does any later
+    iteration of the same step call.  bpgl_solver_status re-runs the lost iterations on the
+    two-pass kernels for the rest of the solve.  The test hook "onepass_fail_at" makes the launch
+    of iteration t report such a failure (once).  Result: the reference fixture within 1e-9 and
+    the reference's err_iter trace, as every solver test; the next solve runs one pass again."""
+    fx = golden("c1_b1_p1_f32in")
+    A = oracle.fixture_A(fx)
+    IT = int(fx["ITER_MAX"])
+    gc = make_cls("float")(A, 1, device=0)
+    gc.set_tuning("onepass", 1)
+    gc.set_tuning("onepass_fail_at", fail_at)
+    res = gc.run(fx["b"], float(fx["mu"]), IT, record=True, use_graph=use_graph)
+    assert gc.solver_stat("fallbacks") == 1 and gc.solver_stat("onepass") == 0
+    assert res["iters"] == IT and res["t_last"] == IT - 1
+    assert rel(res["x"], fx["x"]) <= 1e-9, rel(res["x"], fx["x"])
+    np.testing.assert_allclose(res["err_iter"][:IT], fx["err_iter"][:IT], rtol=1e-6, atol=1e-9)
+    again = gc.run(fx["b"], float(fx["mu"]), IT)
+    assert gc.solver_stat("fallbacks") == 0 and gc.solver_stat("onepass") == 1
+    assert rel(again["x"], res["x"]) <= 1e-10, rel(again["x"], res["x"])
+
+
+def test_failure_state_is_frozen_until_status():
+    """iterations after a failed launch leave x, the residual and t untouched until the status
+    call recovers them (split step calls, a failure in the middle of an 8-iteration graph)"""
+    rs = np.random.RandomState(17)
+    A = rs.randn(700, 9000)
+    b = rs.randn(700)
+    mu = 0.05 * float(np.abs(A.T @ b).max())
+    gc = make_cls("float")(A, 1, device=0)
+    clean = gc.run(b, mu, 60)
+    gc.set_tuning("onepass_fail_at", 20)
+    gc.solver_reset(b, mu)
+    gc.solver_step(20)
+    gc.stream.synchronize()
+    x20 = gc._x.clone()
+    r20 = gc._ctx_residual().clone()
+    gc.solver_step(24)                 # iteration 20 fails: iterations 20..43 commit nothing
+    gc.stream.synchronize()
+    assert torch.equal(gc._x, x20) and torch.equal(gc._ctx_residual(), r20)
+    st = gc.solver_status()            # recovers 20..43 on the two-pass kernels
+    assert st["iters"] == 44 and gc.solver_stat("fallbacks") == 1
+    gc.solver_step(16)
+    assert gc.solver_status()["iters"] == 60
+    assert rel(gc.solver_x(), clean["x"]) <= 1e-10, rel(gc.solver_x(), clean["x"])
+
+
+def test_contention_with_a_concurrent_kernel():
+    """the real failure mode: long GEMMs on another stream hold CUs while the solver runs.
+    Whether or not a hand-off runs out of polls (it depends on the scheduler), the solve
+    finishes with every iteration applied and the same iterates as an undisturbed run to
+    rounding (a fallback changes the summation path: <= 1e-9)"""
+    rs = np.random.RandomState(23)
+    A = rs.randn(2048, 65536) / 256.0
+    b = rs.randn(2048)
+    mu = 0.05 * float(np.abs(A.T @ b).max())
+    gc = make_cls("float")(A, 1, device=0)
+    clean = gc.run(b, mu, 300)
+    hog = torch.cuda.Stream(device=0)
+    X = torch.randn(8192, 8192, device="cuda:0")
+    with torch.cuda.stream(hog):
+        for _ in range(12):
+            X = torch.tanh(X @ X * 1e-4)
+    gc.solver_reset(b, mu)
+    gc.solver_step(300)
+    st = gc.solver_status()
+    torch.cuda.synchronize()
+    print(f"contention: fallbacks {gc.solver_stat('fallbacks')}, iters {st['iters']}")
+    assert st["iters"] == 300
+    assert rel(gc.solver_x(), clean["x"]) <= 1e-9, rel(gc.solver_x(), clean["x"])

@@ -247,3 +247,79 @@ def test_two_granules_ragged_width_with_records():
     # times of the completed iterations increase; the stopping iteration records none, as the
     # reference breaks before time_record (lasso.py:147-157)
     assert np.all(np.diff(one["time_iter"][:T]) > 0) and one["time_iter"][T] == 0.0
+
+
+def test_rccl_rows_failure_is_retried():
+    """row shards: a failed k_onepass launch (test hook "onepass_fail_at") raises the failure
+    slot of the exchange, so every rank skips that iteration and the ones after it; the status
+    call re-runs them on the one-pass kernels (row shards have no two-pass iteration).  Same
+    iterates as an undisturbed run to rounding (the refresh cadence follows the enqueued count,
+    so the exact-gradient refreshes land elsewhere: <= 1e-10)"""
+    rs = np.random.RandomState(8)
+    m, n = 1500, 12000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    rows.set_tuning("exchange_fp32", 0)
+    clean = rows.run(b, mu, 150)
+    for fp32 in (0, -1):
+        rows.set_tuning("exchange_fp32", fp32)
+        rows.set_tuning("onepass_fail_at", 45)
+        res = rows.run(b, mu, 150)
+        assert res["iters"] == 150
+        assert rows.solver_stat("retries") == 150 - 45 and rows.solver_stat("onepass") == 1
+        tol = 1e-10 if fp32 == 0 else 1e-6
+        assert rel(res["x"], clean["x"]) <= tol, (fp32, rel(res["x"], clean["x"]))
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_external_rows_failure_on_one_rank(fp32):
+    """caller-side exchange: rank 0's launch fails at t = 5; the summed failure slot makes both
+    ranks skip the iteration, bpgl_solver_status reports BPGL_E_EXCHANGE on every rank with the
+    state intact, and the caller re-runs the iteration.  x stays bit-identical across ranks and
+    within 1e-12 of the undisturbed run (the re-run launch walks its rows in the other direction,
+    launches alternate it, so the U partial sums change order)"""
+    rs = np.random.RandomState(21)
+    m, n = 1001, 5000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.1, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    ref = run_external(A, b, mu, 2, 40, fp32=fp32)
+    ranks = []
+    for g in range(2):
+        gc = make_cls("float")(D.shard_rows(A, g, 2), 1, device=0, shard="rows")
+        gc.set_ranks(g, 2)
+        gc.set_tuning("onepass_refresh", 64)
+        gc.set_tuning("exchange_fp32", 1 if fp32 else 0)
+        ranks.append(gc)
+    ranks[0].set_tuning("onepass_fail_at", 5)
+    diag = sum(gc._diag.clone() for gc in ranks)
+    for g, gc in enumerate(ranks):
+        gc.set_diag(diag)
+        s, e = D.row_bounds(m, g, 2)
+        gc.solver_reset(np.asarray(b).reshape(-1)[s:e], mu, use_graph=False)
+    for gc in ranks:
+        gc.solver_phase(2)
+    _exchange(ranks)
+    for gc in ranks:
+        gc.solver_phase(3)
+
+    def one_iteration():
+        for gc in ranks:
+            gc.solver_phase(0)
+        _exchange(ranks, fp32)
+        for gc in ranks:
+            gc.solver_phase(1)
+
+    for t in range(40):
+        one_iteration()
+        if t == 5:
+            for gc in ranks:
+                with pytest.raises(N.BpglError, match="state is intact"):
+                    gc.solver_status()
+            one_iteration()            # the lost iteration again
+    xs = [gc.solver_x() for gc in ranks]
+    np.testing.assert_array_equal(xs[0], xs[1])
+    assert rel(xs[0], ref[0].solver_x()) <= 1e-12, rel(xs[0], ref[0].solver_x())
+    assert all(gc.solver_status()["iters"] == 40 for gc in ranks)
