@@ -87,3 +87,22 @@ def test_sharded_decomposition_equals_single(golden):
     a = oracle.run(A, fx["b"], fx["mu"], 1, 100, P=1)
     b = oracle.run(A, fx["b"], fx["mu"], 1, 100, P=8)
     assert np.linalg.norm(a["x"] - b["x"]) <= 1e-10 * np.linalg.norm(a["x"])
+
+
+def test_dropin_run_of_reference_driver_is_bitwise():
+    """tests/golden/dropin/*.npz: the reference's unmodified ClassLassoCPU (lasso.py:25-169, its
+    Pool included) run with sys.modules["cpu_calculation"] bound to this repository's
+    convex_optimization_amd.cpu_calculation (tests/golden/dropin_proof.py, build container only).
+    Every array -- x, err_iter, t_last, the block order, d_ATA, b, mu -- equals the fixture of the
+    run on the reference's own cpu_calculation.py bit for bit."""
+    import os
+    import numpy as np
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    names = sorted(f for f in os.listdir(os.path.join(here, "dropin")) if f.endswith(".npz"))
+    assert len(names) == 7
+    for name in names:
+        a = np.load(os.path.join(here, "dropin", name))
+        b = np.load(os.path.join(here, name))
+        assert sorted(a.files) == sorted(b.files)
+        for k in b.files:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"{name}:{k}")
