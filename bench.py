@@ -277,19 +277,19 @@ def measure(ctx, args, m, n_total):
     times, samples = gc.kernel_times()
     gc.set_kernel_timing(False)
     refresh_ms = times["refresh"] * samples / n_ref_ev if n_ref_ev else 0.0
-    period = gc.solver_stat("refresh_period")
     refresh_ms = ctx.max(refresh_ms)
     st = gc.solver_status()   # completes any iteration a failed one-pass launch lost (outside the windows)
+    period = gc.solver_stat("refresh_period")
     # graph windows; after each, the status call (outside the window) would re-run iterations a
     # failed one-pass launch lost -- such a window did not do its K iterations and is dropped
     wins = []
     for _ in range(args.windows):
         r0 = gc.solver_stat("refreshes")
-        rec0 = gc.solver_stat("fallbacks") + gc.solver_stat("retries")
+        rec0 = gc.solver_stat("fallbacks")
         el = timed_window(ctx, sync, gc.solver_step, args.steps)
         n_ref = ctx.max(gc.solver_stat("refreshes") - r0)
         st = gc.solver_status()
-        lost = ctx.max(gc.solver_stat("fallbacks") + gc.solver_stat("retries") - rec0) > 0
+        lost = ctx.max(gc.solver_stat("fallbacks") - rec0) > 0
         adj = el - n_ref * refresh_ms * 1e-3 + (args.steps / period * refresh_ms * 1e-3 if period else 0.0)
         wins.append({"s": el, "refreshes": int(n_ref), "s_amortised": adj, "lost_iterations": bool(lost)})
     if all(w["lost_iterations"] for w in wins):
@@ -297,7 +297,7 @@ def measure(ctx, args, m, n_total):
     assert st["iters"] == args.warmup + n_ev + args.windows * args.steps or st["stopped"], st
     return dict(gc=gc, windows=wins, el_events=el_ev, n_events=n_ev, kernel_ms=times, samples=samples, status=st,
                 refresh_ms=refresh_ms, refresh_period=period, w_local=gc.MAT_WIDTH, m_local=gc.MAT_HEIGHT,
-                b=b, mu=mu, fallbacks=gc.solver_stat("fallbacks"), retries=gc.solver_stat("retries"))
+                b=b, mu=mu, fallbacks=gc.solver_stat("fallbacks"), onepass=gc.solver_stat("onepass"))
 
 
 def host_cores():
@@ -658,7 +658,7 @@ def main():
             "ms_per_step_raw_median": el_raw / K * 1e3,
             "refresh": {"period": res["refresh_period"], "ms_per_refresh": res["refresh_ms"],
                         "folded": "window time - refreshes inside x ms_per_refresh + K/period x ms_per_refresh"},
-            "onepass_recoveries": {"fallbacks": res["fallbacks"], "retries": res["retries"]},
+            "onepass_fallbacks": res["fallbacks"],
             "fused": args.fused,
             "iters_per_s_eager_with_events": iters_s_ev,
             "kernel_avg_ms": kms,

@@ -105,8 +105,7 @@ struct bpgl_ctx {
     int64_t op_fail_at = -1;   // test hook "onepass_fail_at": the launch of this iteration reports a failure
     // counters since the solver reset (bpgl_solver_stat)
     int64_t n_refresh = 0;     // exact-gradient refreshes enqueued
-    int64_t n_fallback = 0;    // one-rank one-pass solves moved to the two-pass kernels after a failure
-    int64_t n_retry = 0;       // row-shard one-pass iterations re-run after a failure
+    int64_t n_fallback = 0;    // one-pass solves moved to the two-pass kernels after a failure
     OnePassArgs op{};
 };
 
@@ -355,13 +354,14 @@ int onepass_launch(bpgl_ctx* c) {
 }
 // the one-pass tail's view of U: the row-group partials (one rank), or the all-reduced sum
 // in the exchange buffer (row shards)
-// Row shards exchange [U | r.s23 | s23.s23] in fp32 (U rounded, the scalars as hi + lo pairs):
-// half the all-reduce bytes; measured drift DESIGN.md section 6 (1.8e-7 with one rank, 1.5e-6
-// with eight: each rank's partial is rounded before the cross-rank cancellation), so it is
-// opt-in: 1 = any row-shard exchange, -1 = RCCL communicators only, 0 (default) = fp64.  The
-// exact-gradient refresh is always fp64.
+// Row shards exchange [U | r.s23 | s23.s23 | failed] in fp32 (U rounded, the scalars as hi + lo
+// pairs, exact to ~2^-48 for one rank; summed over several ranks RCCL rounds each hi and lo sum
+// to fp32, so the scalars are then fp32-accurate): half the all-reduce bytes; measured drift
+// DESIGN.md section 6 (1.8e-7 with one rank, 1.5e-6 with eight: each rank's partial is rounded
+// before the cross-rank cancellation), so it is opt-in: 1 = any row-shard exchange, -1 = RCCL
+// communicators only, 0 (default) = fp64.  The exact-gradient refresh is always fp64.
 bool xch_f32(const bpgl_ctx* c) {
-    return c->rows && (c->xch32 > 0 || (c->xch32 < 0 && c->comm && !c->external));
+    return c->rows && c->op_on && (c->xch32 > 0 || (c->xch32 < 0 && c->comm && !c->external));
 }
 OnePassArgs op_tail_args(const bpgl_ctx* c) {
     OnePassArgs o = c->op;
@@ -396,7 +396,6 @@ int onepass_local_gradient(bpgl_ctx* c, double* dst) {
 // exact g = A^T r into G (at reset and every op_refresh iterations); row shards sum it over ranks
 int onepass_refresh(bpgl_ctx* c) {
     int rc;
-    c->n_refresh++;
     if ((rc = onepass_local_gradient(c, c->op.G))) return rc;
     if (c->rows && c->comm && (rc = allreduce_sum(c, c->op.G, c->wp))) return rc;
     return onepass_tail<false>(c);   // the shrink of the next iteration from the exact g
@@ -533,6 +532,43 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
     return 0;
 }
 
+// Row shards on the two-pass kernels (RCCL ranks; after a failed one-pass hand-off, or with
+// "onepass" = 0): phase 0 = the exact g = sum_q A_q^T r_q (colpass, colreduce, all-reduce of
+// w_pad) and the shrink, s23_q = A_q D on the local rows (rowpass, rowreduce), the line-search
+// partials and ONE all-reduce of [r.s23 | s23.s23 | failed] (3 fp64); phase 1 = k_onepass_tail
+// (the line search at its head; U = 0).  Two passes over A_q and two all-reduces per iteration,
+// but no co-residency requirement.
+int enqueue_phase_rows_twopass(bpgl_ctx* c, int64_t it, int phase) {
+    int rc;
+    if (phase == 0) {
+        ev_record(c, it, 0, 0);
+        if ((rc = onepass_refresh(c))) return rc;     // exact g, then the shrink (tail<false>)
+        ev_record(c, it, 0, 1);
+        ev_record(c, it, 2, 0);
+        if ((rc = rowpass(c, c->p.D, c->p.slab_s, -1))) return rc;
+        const dim3 g(rowreduce_blocks(c)), b(kThreads);
+        if (c->p.nseg <= 4) hipLaunchKernelGGL(k_rowreduce<1>, g, b, 0, c->stream, c->p, c->p.slab_s, c->op.S, 1);
+        else if (c->p.nseg <= 16) hipLaunchKernelGGL(k_rowreduce<4>, g, b, 0, c->stream, c->p, c->p.slab_s, c->op.S, 1);
+        else hipLaunchKernelGGL(k_rowreduce<16>, g, b, 0, c->stream, c->p, c->p.slab_s, c->op.S, 1);
+        LAUNCH_CHECK("k_rowreduce");
+        ev_record(c, it, 2, 1);
+        ev_record(c, it, 3, 0);
+        HIP_TRY(hipMemsetAsync(c->p.comm, 0, 8 * c->wp, c->stream));
+        hipLaunchKernelGGL(k_rows2_fold, dim3(1), dim3(kThreads), 0, c->stream, op_params(c), c->op, c->p.comm,
+                           (int)rowreduce_blocks(c));
+        LAUNCH_CHECK("k_rows2_fold");
+        ev_record(c, it, 3, 1);
+        ev_record(c, it, 4, 0);
+        if (c->comm && (rc = allreduce_sum(c, c->p.comm + c->wp, 3))) return rc;
+        ev_record(c, it, 4, 1);
+    } else {
+        ev_record(c, it, 6, 0);
+        if ((rc = onepass_tail<true>(c))) return rc;
+        ev_record(c, it, 6, 1);
+    }
+    return 0;
+}
+
 int enqueue_phase_onepass(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
     if (c->rows) return enqueue_phase_onepass_rows(c, it, phase);
@@ -551,6 +587,7 @@ int enqueue_phase_onepass(bpgl_ctx* c, int64_t it, int phase) {
 int enqueue_phase(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
     if (c->op_on) return enqueue_phase_onepass(c, it, phase);
+    if (c->rows) return enqueue_phase_rows_twopass(c, it, phase);
     if (c->fused) return enqueue_phase_fused(c, it, phase);
     const bool multi = c->comm != nullptr || c->external;
     if (phase == 0) {
@@ -636,6 +673,7 @@ int step_impl(bpgl_ctx* c, int64_t n_iter) {
     for (int64_t i = 0; i < n_iter;) {
         if (K > 0 && c->op_t > 0 && c->op_t % K == 0) {
             ev_record(c, c->timed_iters, 8, 0);
+            c->n_refresh++;
             if ((rc = onepass_refresh(c))) return rc;
             ev_record(c, c->timed_iters, 8, 1);
         }
@@ -658,12 +696,12 @@ int step_impl(bpgl_ctx* c, int64_t n_iter) {
 
 // A one-pass launch whose row hand-off ran out of polls (its blocks were not all resident:
 // another kernel or process held CUs) commits nothing, and neither does any iteration after
-// it until the flag is cleared (bpgl_onepass.h).  Re-run the iterations that were lost: one
-// rank moves to the two-pass kernels for the rest of this solve (they need no co-residency);
-// row shards run the lost iterations again on the one-pass kernels (every rank sees the same
-// summed failure flag, so every rank re-runs the same iterations; RCCL ranks must all call
-// bpgl_solver_status at the same point), at most kOpRetries times.
-constexpr int kOpRetries = 3;
+// it until the flag is cleared (bpgl_onepass.h).  Re-run the iterations that were lost on the
+// two-pass kernels, which need no co-residency, and stay on them for the rest of this solve:
+// one rank on the ordinary two-pass iteration, RCCL row shards on the two-pass row iteration
+// (every rank sees the same summed failure flag, so every rank switches at the same iteration;
+// RCCL ranks must all call bpgl_solver_status at the same point).  External-exchange ranks
+// get BPGL_E_EXCHANGE with the state intact.
 int read_state(bpgl_ctx* c, DevState& st) {
     HIP_TRY(hipMemcpyAsync(&st, c->p.st, sizeof st, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -671,7 +709,7 @@ int read_state(bpgl_ctx* c, DevState& st) {
 }
 int recover_onepass(bpgl_ctx* c, DevState& st) {
     int rc;
-    for (int attempt = 0; st.op_fail; ++attempt) {
+    while (st.op_fail) {
         HIP_TRY(hipMemsetAsync(&c->p.st->op_fail, 0, sizeof st.op_fail, c->stream));
         const int64_t t = st.t;
         c->op_fail_at = -1;   // the test hook fires once
@@ -680,16 +718,11 @@ int recover_onepass(bpgl_ctx* c, DevState& st) {
             return fail(BPGL_E_EXCHANGE, "one-pass row hand-off timed out (blocks not co-resident); iterations from "
                                          "t = %lld on were not applied and the solver state is intact: run them again",
                         (long long)t);
-        if (c->rows && attempt >= kOpRetries)
-            return fail(BPGL_E_EXCHANGE, "one-pass row hand-off timed out %d times in a row at t = %lld (another "
-                                         "kernel keeps CUs busy); the solver state is intact at t", kOpRetries + 1,
+        if (!c->op_on)   // cannot happen: only k_onepass raises the flag
+            return fail(BPGL_E_EXCHANGE, "hand-off failure flag set outside the one-pass iteration at t = %lld",
                         (long long)t);
-        if (c->rows) {
-            c->n_retry += c->req_t - t;
-        } else {
-            c->op_on = false;
-            c->n_fallback++;
-        }
+        c->op_on = false;
+        c->n_fallback++;
         if ((rc = capture_graphs(c))) return rc;
         if (!st.done && c->req_t > t && (rc = step_impl(c, c->req_t - t))) return rc;
         if ((rc = read_state(c, st))) return rc;
@@ -1045,7 +1078,10 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
     {
         const char* why = c->onepass != 0 ? onepass_ineligible(c) : "disabled";
         if (c->onepass == 1 && why) return fail(BPGL_E_ARG, "onepass=1: %s", why);
-        if (c->rows && why) return fail(BPGL_E_ARG, "row shards run the one-pass iteration only: %s", why);
+        // row shards without one pass: the two-pass row iteration (RCCL ranks only; it needs the
+        // geometry of a one-pass-shaped context for its buffers)
+        if (c->rows && why && (c->external || !c->op_shape))
+            return fail(BPGL_E_ARG, "external row shards run the one-pass iteration only: %s", why);
         c->op_on = c->onepass != 0 && !why;
         c->op_t = 0;
         c->op_refresh_pending = false;
@@ -1055,7 +1091,7 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
     c->use_graph = use_graph != 0 && !c->external;
     if ((rc = capture_graphs(c))) return rc;
     c->req_t = 0;
-    c->n_refresh = c->n_fallback = c->n_retry = 0;
+    c->n_refresh = c->n_fallback = 0;
     c->solver = true;
     c->timed_iters = 0;
     return 0;
@@ -1094,7 +1130,6 @@ int bpgl_solver_stat(bpgl_ctx* c, const char* key, int64_t* value) {
     else if (!strcmp(key, "refresh_period")) *value = c->op_on ? c->op_refresh : 0;
     else if (!strcmp(key, "refreshes")) *value = c->n_refresh;
     else if (!strcmp(key, "fallbacks")) *value = c->n_fallback;
-    else if (!strcmp(key, "retries")) *value = c->n_retry;
     else if (!strcmp(key, "requested")) *value = c->req_t;
     else if (!strcmp(key, "enqueued")) *value = c->op_t;
     else return fail(BPGL_E_ARG, "unknown stat '%s'", key);

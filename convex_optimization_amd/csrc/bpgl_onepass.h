@@ -422,6 +422,37 @@ __global__ __launch_bounds__(kThreads) void k_onepass_fold(Params p, OnePassArgs
     }
 }
 
+// Row shards without the one-pass kernel (a failed hand-off, or "onepass" = 0): the line-search
+// scalars of the two-pass row iteration -- the fixed-order sums of k_rowreduce's per-block
+// [r.s23, s23.s23] partials -- into the exchange tail [.. | r.s23 | s23.s23 | failed = 0], and
+// the fixed-order fold of the shrink partials for the line search at the head of
+// k_onepass_tail (the U part of the buffer is zero: the next iteration recomputes g exactly).
+// One block.
+__global__ __launch_bounds__(kThreads) void k_rows2_fold(Params p, OnePassArgs o, double* __restrict__ out,
+                                                         int nrr) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double rs = 0.0, ss = 0.0;
+    for (int k = threadIdx.x; k < nrr; k += kThreads) {
+        rs += p.parts2[2ll * k];
+        ss += p.parts2[2ll * k + 1];
+    }
+    __shared__ double sr[kWaves], sq[kWaves];
+    rs = wave_sum(rs);
+    ss = wave_sum(ss);
+    if (lane == 0) { sr[wave] = rs; sq[wave] = ss; }
+    __syncthreads();
+    double a, b, e;
+    fold_parts(p, p.nparts, a, b, e);
+    if (threadIdx.x == 0) {
+        out[p.wp] = ((sr[0] + sr[1]) + sr[2]) + sr[3];
+        out[p.wp + 1] = ((sq[0] + sq[1]) + sq[2]) + sq[3];
+        out[p.wp + 2] = 0.0;
+        o.abe[0] = a;
+        o.abe[1] = b;
+        o.abe[2] = e;
+    }
+}
+
 // rec = 1 / diag after the column norms were summed over row shards (lasso.py:29-30)
 __global__ __launch_bounds__(kThreads) void k_recip(const double* __restrict__ d, double* __restrict__ rec,
                                                     long long n) {

@@ -430,7 +430,7 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else if (!strcmp(key, "defer_x")) {
         if (value != 0 && value != 1) return fail(BPGL_E_ARG, "defer_x must be 0 or 1");
         c->defer_x = (int)value;
-        c->solver = false;   // the two forms keep different state (Ax): a reset must follow
+        c->solver = false;   // the graph bakes in where x is updated (and the flush): a reset must follow
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;

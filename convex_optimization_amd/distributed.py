@@ -15,7 +15,7 @@ Row shards (``shard="rows"``, one feature block; no reference counterpart):
 rank g holds rows ``row_bounds(m, g, G)`` of A, its rows of b and of the
 residual, and a replicated x.  Every iteration streams the local A once
 (k_onepass: s23_g = A_g D and U_g = A_g^T s23_g together), and ONE all-reduce
-(SUM) of w_pad + 2 fp64 [U | r.s23 | s23.s23] gives every rank the identical
+(SUM) of w_pad + 3 fp64 [U | r.s23 | s23.s23 | failed] gives every rank the identical
 gradient update g += gamma U and step size.  Column shards need A read twice
 per iteration (the exchange of s23 sits between the two products); row shards
 trade that second pass for a w-sized exchange, which is the better deal on
@@ -77,8 +77,9 @@ def shard_rows(A, rank, nranks):
 
 
 def row_exchange_layout(wp):
-    """Offsets in the row-shard all-reduce buffer (SUM over ranks)."""
-    return dict(u=(0, wp), rs=wp, ss=wp + 1, count=wp + 2)
+    """Offsets in the row-shard all-reduce buffer (SUM over ranks); `failed` carries each rank's
+    one-pass failure flag (a nonzero sum makes every rank skip the iteration)."""
+    return dict(u=(0, wp), rs=wp, ss=wp + 1, failed=wp + 2, count=wp + 3)
 
 
 def assemble_x(x_shards, Block):

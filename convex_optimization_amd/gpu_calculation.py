@@ -267,7 +267,7 @@ class GPU_Calculation:
 
     def solver_stat(self, key):
         """Counter since the last reset (include/bpgl.h bpgl_solver_stat): "onepass", "refreshes",
-        "fallbacks", "retries", "requested", "enqueued"."""
+        "fallbacks", "requested", "enqueued", "refresh_period"."""
         v = ctypes.c_int64()
         N.check(N.lib().bpgl_solver_stat(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_solver_stat")
         return v.value

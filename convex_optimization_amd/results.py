@@ -6,8 +6,8 @@ compare.py:7-10 loads four 1-D float text files from ``settings.Dir_PERFORMANCE`
 plots log10(error) against time (compare.py:12-21).  Nothing in the reference
 writes them; ``save_performance`` does, from a driver's ``time_iter`` /
 ``err_iter`` arrays (lasso.py:54-62), and ``compare_figure`` draws compare.py's
-figure into a file.  ``list_aver`` is average.py:6-24 (column mean of ragged
-lists, for several instances).
+figure into a file.  (average.py, which averages records over instances, is out of
+scope: SURVEY.md section 2.)
 """
 import os
 
@@ -71,13 +71,3 @@ def compare_figure(directory=None, out_path=None):
     plt.close(fig)
     return out_path
 
-
-def list_aver(perform):
-    """Column mean over ragged sequences, each column averaged over the sequences long enough."""
-    longest = max((len(p) for p in perform), default=0)
-    out = []
-    for i in range(longest):
-        vals = [p[i] for p in perform if i < len(p)]
-        if vals:
-            out.append(sum(vals) / len(vals))
-    return out

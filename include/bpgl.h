@@ -41,11 +41,11 @@ enum {
     BPGL_E_RCCL = -4,     /* RCCL error                                  */
     BPGL_E_SCRATCH = -5,  /* scratch buffer too small                    */
     BPGL_E_EXCHANGE = -6  /* one-pass row hand-off timed out (another
-                             kernel held CUs) and could not be recovered
-                             (external-exchange ranks, or row shards that
-                             failed kOpRetries + 1 times in a row); the
-                             failed iterations committed nothing: the
-                             solver state is intact at the reported t     */
+                             kernel held CUs) on an external-exchange
+                             rank; the failed iterations committed
+                             nothing: the solver state is intact at the
+                             reported t (other ranks recover, see
+                             bpgl_solver_status)                          */
 };
 
 typedef struct bpgl_ctx bpgl_ctx;
@@ -177,13 +177,15 @@ double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
  *   stopped flag, last t, last step size, last error).  It also completes
  *   iterations a one-pass launch lost: a launch whose blocks were not all
  *   resident (another kernel or process held CUs) commits nothing, nor does
- *   any later iteration until this call re-runs them -- one rank on the
- *   two-pass kernels for the rest of the solve, row shards on the one-pass
- *   kernels again (RCCL row-shard ranks must all call it at the same point).
+ *   any later iteration until this call re-runs them on the two-pass kernels,
+ *   which stay in use for the rest of the solve (RCCL row shards: the two-pass
+ *   row iteration, two passes over the local rows and two all-reduces per
+ *   iteration; every rank switches at the same iteration, so RCCL row-shard
+ *   ranks must all call it at the same point).
  * bpgl_solver_stat: counters since the last reset -- "onepass" (1 while the
  *   one-pass iteration is in use), "refresh_period" (iterations between
  *   exact-gradient refreshes, 0 = none), "refreshes" (exact-gradient refreshes
- *   enqueued), "fallbacks" / "retries" (recoveries above), "requested"
+ *   enqueued), "fallbacks" (recoveries above), "requested"
  *   (iterations asked of bpgl_solver_step), "enqueued".
  * bpgl_solver_residual: device pointer of the residual s11 = sum_k Ax_k - b (m).
  */

@@ -132,13 +132,16 @@ def test_row_bounds_cover_and_balance():
         D.row_bounds(3, 0, 4)
     A = np.arange(20.0).reshape(5, 4)
     np.testing.assert_array_equal(np.concatenate([D.shard_rows(A, g, 2) for g in range(2)]), A)
-    assert D.row_exchange_layout(16) == dict(u=(0, 16), rs=16, ss=17, count=18)
+    assert D.row_exchange_layout(16) == dict(u=(0, 16), rs=16, ss=17, failed=18, count=19)
 
 
-def _row_rank_iterations(A_loc, b_loc, mu, iters, refresh):
+def _row_rank_iterations(A_loc, b_loc, mu, iters, refresh, fail_at=None):
     """One rank of the row-sharded one-pass solver, restating the device kernels' per-rank
-    work (k_onepass, k_onepass_fold, k_linesearch, k_onepass_tail; colpass + all-reduce for the
-    exact gradient) with the gloo all-reduce standing in for RCCL."""
+    work (k_onepass, k_onepass_fold, k_onepass_tail with the line search at its head; colpass +
+    all-reduce for the exact gradient) with the gloo all-reduce standing in for RCCL.
+    ``fail_at``: this rank's launch of that iteration reports a hand-off failure once; the
+    summed `failed` slot makes every rank skip the iteration, which is then run again (what
+    bpgl_solver_status does for RCCL row shards)."""
     def allreduce(v):
         t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64))
         dist.all_reduce(t)
@@ -157,7 +160,8 @@ def _row_rank_iterations(A_loc, b_loc, mu, iters, refresh):
         return bx, bx - x
     bx, Dv = shrink(g, x)
     lay = D.row_exchange_layout(w)
-    for t in range(iters):
+    t = 0
+    while t < iters:
         if refresh and t and t % refresh == 0:
             g = allreduce(A_loc.T @ r)
             bx, Dv = shrink(g, x)
@@ -166,7 +170,13 @@ def _row_rank_iterations(A_loc, b_loc, mu, iters, refresh):
         buf[:w] = A_loc.T @ s23
         buf[lay["rs"]] = r @ s23
         buf[lay["ss"]] = s23 @ s23
+        buf[lay["failed"]] = 1.0 if t == fail_at else 0.0
+        if t == fail_at:
+            fail_at = None                      # the failure happens once
         buf = allreduce(buf)
+        if buf[lay["failed"]] != 0.0:           # every rank skips, then runs the iteration again
+            continue
+        t += 1
         r1 = buf[lay["rs"]] + mu * (np.abs(bx).sum() - np.abs(x).sum())
         r2 = buf[lay["ss"]]
         gamma = 0.0 if r2 == 0 else min(max(-r1 / r2, 0.0), 1.0)
@@ -183,8 +193,10 @@ def _row_solver_worker(rank, world, port, out):
     fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "c1_b1_p1_f32in.npz")))
     A = oracle.fixture_A(fx)
     s, e = D.row_bounds(A.shape[0], rank, world)
-    out[rank] = _row_rank_iterations(D.shard_rows(A, rank, world), fx["b"].reshape(-1)[s:e],
-                                     float(fx["mu"]), 120, refresh=50).tolist()
+    args = (D.shard_rows(A, rank, world), fx["b"].reshape(-1)[s:e], float(fx["mu"]), 120)
+    out[rank] = _row_rank_iterations(*args, refresh=50).tolist()
+    # rank 1's launch of iteration 37 fails: both ranks skip it and run it again
+    out[("failed", rank)] = _row_rank_iterations(*args, refresh=50, fail_at=37 if rank == 1 else None).tolist()
     dist.destroy_process_group()
 
 
@@ -197,3 +209,6 @@ def test_row_sharded_exchange_protocol_matches_reference():
     ref = oracle.run(A, fx["b"], float(fx["mu"]), 1, 120)["x"]
     np.testing.assert_array_equal(np.array(out[0]), np.array(out[1]))   # x replicated bit for bit
     assert np.linalg.norm(np.array(out[0]) - ref) <= 1e-9 * np.linalg.norm(ref)
+    # a failure on one rank: the same iterates bit for bit, on both ranks
+    np.testing.assert_array_equal(np.array(out[("failed", 0)]), np.array(out[0]))
+    np.testing.assert_array_equal(np.array(out[("failed", 1)]), np.array(out[0]))

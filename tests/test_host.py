@@ -115,8 +115,3 @@ def test_results_files_roundtrip_and_figure(tmp_path):
     png = results.compare_figure(str(tmp_path))
     assert (tmp_path / "compare.png").exists() and png.endswith("compare.png")
 
-
-def test_list_aver_matches_reference_semantics():
-    from convex_optimization_amd.results import list_aver
-    assert list_aver([[1, 2, 3], [3, 4], [5]]) == [3.0, 3.0, 3.0]
-    assert list_aver([]) == []

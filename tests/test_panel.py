@@ -169,9 +169,10 @@ def test_panel_rejects_bad_shapes():
 
 @pytest.mark.parametrize("d_split", [2, 1])
 def test_panel_deferred_x_update_agrees(d_split):
-    """One block: x += gamma D' applied in the next pass-1 epilogue (defer_x 1, R updated
-    incrementally) vs in the update kernel (defer_x 0, R = Ax - B): the same iterates up to
-    the fp64 rounding of R (split-K-like tolerance); x is current after every step call."""
+    """One block: where the x update is placed -- x += gamma D' applied in the next pass-1
+    epilogue (defer_x 1) or in the update kernel (defer_x 0).  With one feature block both
+    forms update the residual the same way (R += gamma S), so this compares the placement of
+    the x update only: the same iterates to rounding; x is current after every step call."""
     Ab, B, mu = instance(512, 1024, 32, seed=13)
     out = {}
     for dx in (0, 1):
