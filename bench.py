@@ -93,6 +93,8 @@ def parse():
                     help="iterations per timed window (default 256)")
     ap.add_argument("--warmup", type=int, default=200,
                     help="untimed iterations before the windows (default 200)")
+    ap.add_argument("--ramp", type=int, default=512,
+                    help="minimum length of the eager window with per-kernel events (default 512 iterations)")
     ap.add_argument("--windows", type=int, default=5,
                     help="timed windows of exactly --steps iterations; value uses the median (default 5)")
     ap.add_argument("--m", type=int, default=M)
@@ -126,6 +128,10 @@ def parse():
     ap.add_argument("--d-split", type=int, default=-1, choices=[-1, 1, 2],
                     help="panel path: the direction enters the A D pass as a hi + lo bf16 pair (2) or as its "
                          "bf16 rounding (1); -1: library default")
+    ap.add_argument("--waves1", type=int, default=-1, choices=[-1, 0, 4],
+                    help="panel path, pass 1: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
+    ap.add_argument("--waves2", type=int, default=-1, choices=[-1, 0, 4],
+                    help="panel path, pass 2: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
     ap.add_argument("--write-through", type=int, default=-1,
                     help="panel path: write-through store sites mask (1 pass-1 epilogue, 2 pass-2 slab, 4 S, "
                          "8 R; -1: library default)")
@@ -269,7 +275,7 @@ def measure(ctx, args, m, n_total):
     gc.solver_step(args.warmup)
     sync()
     # eager window: kernel averages (events on the solver stream) + clock ramp
-    n_ev = max(args.steps, 512)
+    n_ev = max(args.steps, args.ramp)
     gc.set_kernel_timing(True)
     r0 = gc.solver_stat("refreshes")
     el_ev = timed_window(ctx, sync, gc.solver_step, n_ev)
@@ -478,6 +484,9 @@ def main_panel(args):
         pl.set_tuning("defer_x", args.defer_x)
     if args.write_through >= 0:
         pl.set_tuning("write_through", args.write_through)
+    for q in (1, 2):
+        if getattr(args, f"waves{q}") >= 0:
+            pl.set_tuning(f"waves{q}", getattr(args, f"waves{q}"))
     d_split = pl.get_tuning("d_split")
     del A
     Ab = pl.A_bf16.float()
@@ -494,7 +503,7 @@ def main_panel(args):
     pl.solver_reset(B, mu, use_graph=True)
     pl.solver_step(args.warmup)
     sync()
-    n_ev = max(args.steps, 512)          # eager window: kernel averages + clock ramp
+    n_ev = max(args.steps, args.ramp)          # eager window: kernel averages + clock ramp
     pl.set_kernel_timing(True)
     el_ev = timed_window(ctx, sync, pl.solver_step, n_ev)
     kms, samples = pl.kernel_times()
@@ -525,6 +534,7 @@ def main_panel(args):
             "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
             "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
+            "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
             "defer_x": pl.get_tuning("defer_x"),
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,

@@ -43,10 +43,13 @@ constexpr int kPanelNA = 3;       // A-side stage buffers (two stages in flight)
 constexpr int kPanelNO = 2;       // k-wide-side stage buffers
 constexpr int kPanelAStage = kPanelRows * kPanelK * 2;   // 32 KiB
 
-// NS: bf16 pieces of the k-wide operand (2: hi + lo, ~16-bit mantissa; 1: hi only)
-template <int NT, int NS = 2>
+// NS: bf16 pieces of the k-wide operand (2: hi + lo, ~16-bit mantissa; 1: hi only).
+// WNX: waves along the RHS (0: 2 when NT >= 2, i.e. 8 waves = 2 per SIMD; 4: 16 waves = 4 per
+// SIMD with half the accumulators each -- the "waves" tuning knob)
+template <int NT, int NS = 2, int WNX = 0>
 struct PanelGeo {
-    static constexpr int WN = NT >= 2 ? 2 : 1;        // waves along the RHS
+    static constexpr int WN = WNX ? WNX : (NT >= 2 ? 2 : 1);   // waves along the RHS
+    static_assert(NT % WN == 0, "N-tiles per wave");
     static constexpr int NTW = NT / WN;               // N-tiles per wave
     static constexpr int NW = 4 * WN;                 // waves per block
     static constexpr int T = 64 * NW;                 // threads per block
@@ -157,10 +160,10 @@ __device__ __forceinline__ int swz512(int r, int c) { return c ^ (2 * ((r & 3) |
 // this wave (a piece = 8 image rows of 128 B).  When the stage has fewer pieces than waves
 // (NS = 1 at k = 16 or 32) the spare waves issue nothing: the stage's counted wait only
 // assumes that a wave's A pieces are its youngest operations, which still holds.
-template <int NT, int NS>
+template <int NT, int NS, int WNX>
 __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__ hi, const __bf16* __restrict__ lo,
                                                long long ld, long long ks, char* obuf, int wave, int lane) {
-    using G = PanelGeo<NT, NS>;
+    using G = PanelGeo<NT, NS, WNX>;
     const int pc = q * G::NW + wave;
     if (pc * 8 >= NS * G::K) return;   // wave-uniform
     const int rr = pc * 8 + (lane >> 3);
@@ -169,20 +172,20 @@ __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__
     glds16o((hl ? lo : hi) + (long long)rhs * ld + ks + 8 * c, obuf + pc * 1024);
 }
 // pass-1 A stage: rows ks..ks+63 of A, columns col0..col0+255 -> [64][512 B] (a piece = 2 rows)
-template <int NT>
+template <int NT, int WNX>
 __device__ __forceinline__ void panel_a1_piece(int q, const __bf16* __restrict__ A, long long lda, long long ks,
                                                long long col0, char* abuf, int wave, int lane) {
-    using G = PanelGeo<NT>;
+    using G = PanelGeo<NT, 2, WNX>;
     const int pc = q * G::NW + wave;
     const int row = pc * 2 + (lane >> 5);
     const int c = swz512(row, lane & 31);
     glds16a(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
 }
 // pass-2 A stage: rows r0..r0+255 of A, columns ks..ks+63 -> [256][128 B] (a piece = 8 rows)
-template <int NT>
+template <int NT, int WNX>
 __device__ __forceinline__ void panel_a2_piece(int q, const __bf16* __restrict__ A, long long lda, long long r0,
                                                long long ks, char* abuf, int wave, int lane) {
-    using G = PanelGeo<NT>;
+    using G = PanelGeo<NT, 2, WNX>;
     const int pc = q * G::NW + wave;
     const int row = pc * 8 + (lane >> 3);
     const int c = swz128(row, lane & 7);
@@ -220,12 +223,12 @@ __device__ __forceinline__ bf16x8 panel_afrag1(const char* abuf, int j0, int h, 
 // `a_row0`/`a_col0`: PASS 1 -> (first A row of K, first column of the tile); PASS 2 -> (first row, first column of K).
 // ILV 0: a stage's LDS-DMA pieces are issued together after the barrier; ILV 1: they
 // are spread over the stage's MFMA groups (one scheduling group each).  NS: operand pieces.
-template <int NT, int PASS, int ILV, int NS>
+template <int NT, int PASS, int ILV, int NS, int WNX>
 __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restrict__ A, long long lda,
                                                long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
                                                const __bf16* __restrict__ bl, long long ldb, long long b_k0,
-                                               int nsteps, f32x4 (&acc)[4][PanelGeo<NT>::NTW]) {
-    using G = PanelGeo<NT, NS>;
+                                               int nsteps, f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
+    using G = PanelGeo<NT, NS, WNX>;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
@@ -242,14 +245,14 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
-            panel_op_piece<NT, NS>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
-                                   lane);
+            panel_op_piece<NT, NS, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
+                                        wave, lane);
         } else if (PASS == 1) {
-            panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
-                               abufs + ba * kPanelAStage, wave, lane);
+            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+                                    abufs + ba * kPanelAStage, wave, lane);
         } else {
-            panel_a2_piece<NT>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
-                               abufs + ba * kPanelAStage, wave, lane);
+            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+                                    abufs + ba * kPanelAStage, wave, lane);
         }
     };
     auto issue_a = [&](int s, int buf) {
@@ -322,13 +325,13 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 // reuse is unchanged (a stage's buffers are refilled only after the barrier that follows
 // all of its reads); all LDS-DMA pieces of a stage are issued before its barrier, spread
 // over the first G - 1 groups.
-template <int NT, int PASS, int NS>
+template <int NT, int PASS, int NS, int WNX>
 __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __restrict__ A, long long lda,
                                                     long long a_row0, long long a_col0,
                                                     const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
                                                     long long ldb, long long b_k0, int nsteps,
-                                                    f32x4 (&acc)[4][PanelGeo<NT>::NTW]) {
-    using G = PanelGeo<NT, NS>;
+                                                    f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
+    using G = PanelGeo<NT, NS, WNX>;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
@@ -342,14 +345,14 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
-            panel_op_piece<NT, NS>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
-                                   lane);
+            panel_op_piece<NT, NS, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
+                                        wave, lane);
         } else if (PASS == 1) {
-            panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
-                               abufs + ba * kPanelAStage, wave, lane);
+            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+                                    abufs + ba * kPanelAStage, wave, lane);
         } else {
-            panel_a2_piece<NT>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
-                               abufs + ba * kPanelAStage, wave, lane);
+            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+                                    abufs + ba * kPanelAStage, wave, lane);
         }
     };
     constexpr int NP = G::LO + G::LA;
@@ -464,10 +467,10 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 // epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
 // per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI, int ILV, int DS>
-__global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, int fixed_block,
-                                                                  double* __restrict__ Gout) {
-    using G = PanelGeo<NT>;
+template <int NT, int EPI, int ILV, int DS, int WNX>
+__global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
+                                                                         double* __restrict__ Gout) {
+    using G = PanelGeo<NT, 2, WNX>;
     __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
     const int lane = threadIdx.x & 63;
@@ -476,11 +479,11 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
     if constexpr (ILV == 2)
-        panel_mainloop_pipe<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
-                                      (int)(p.m / kPanelK), acc);
+        panel_mainloop_pipe<NT, 1, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+                                           (int)(p.m / kPanelK), acc);
     else
-        panel_mainloop<NT, 1, ILV, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
-                                      (int)(p.m / kPanelK), acc);
+        panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+                                           (int)(p.m / kPanelK), acc);
 
     // C layout: row = (lane>>4)*4 + r (A column), col = lane & 15 (RHS)
     if (EPI == 0) {
@@ -580,9 +583,9 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass1(PanelParams p, 
 // pass 2: partial S over one column chunk: Sslab[chunk][rhs][row]; the direction in NS
 // bf16 pieces.  grid = (m / 256) x kchunks
 // ---------------------------------------------------------------------------
-template <int NT, int ILV, int NS>
-__global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, int fixed_block) {
-    using G = PanelGeo<NT, NS>;
+template <int NT, int ILV, int NS, int WNX>
+__global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(PanelParams p, int fixed_block) {
+    using G = PanelGeo<NT, NS, WNX>;
     __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
     const int lane = threadIdx.x & 63;
@@ -605,11 +608,11 @@ __global__ __launch_bounds__(PanelGeo<NT>::T) void k_panel_pass2(PanelParams p, 
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
     if constexpr (ILV == 2)
-        panel_mainloop_pipe<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
-                                       chunk * kc, (int)(kc / kPanelK), acc);
+        panel_mainloop_pipe<NT, 2, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
+                                            p.w, chunk * kc, (int)(kc / kPanelK), acc);
     else
-        panel_mainloop<NT, 2, ILV, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
-                                       chunk * kc, (int)(kc / kPanelK), acc);
+        panel_mainloop<NT, 2, ILV, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
+                                            p.w, chunk * kc, (int)(kc / kPanelK), acc);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll

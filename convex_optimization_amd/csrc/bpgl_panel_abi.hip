@@ -33,6 +33,7 @@ struct bpgl_panel {
     int64_t timed_iters = 0;
     bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
     int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
+    int waves[2] = {0, 0};        // waves along the RHS per pass: 0 = 2 (8 waves), 4 = 16 waves ("waves" knobs)
     int dsplit = 2;               // bf16 pieces of the solver's direction (d_split knob)
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
@@ -72,39 +73,46 @@ PanelLayout panel_layout(const bpgl_panel* c) {
 
 // ns: bf16 pieces of the direction (pass 1's epilogue writes it, pass 2 reads it): the
 // solver's d_split knob, 2 for the API products (bpgl_panel_mtm / _mm)
-template <int NT, int ILV, int NS>
+template <int NT, int ILV, int NS, int WNX>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
         case 0:
-            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS>), dim3((unsigned)(c->w / kPanelRows)),
-                                         dim3(PanelGeo<NT>::T), 0, c->stream, c->p, fixed_block, out);
-            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2>), dim3((unsigned)(c->w / kPanelRows)),
-                                    dim3(PanelGeo<NT>::T), 0, c->stream, c->p, fixed_block, out);
+            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX>), dim3((unsigned)(c->w / kPanelRows)),
+                                         dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX>), dim3((unsigned)(c->w / kPanelRows)),
+                                    dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
             LAUNCH_CHECK("k_panel_pass1");
             break;
         case 1:
-            hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
-                               dim3(PanelGeo<NT, NS>::T), 0, c->stream, c->p, fixed_block);
+            hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS, WNX>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
+                               dim3(PanelGeo<NT, NS, WNX>::T), 0, c->stream, c->p, fixed_block);
             LAUNCH_CHECK("k_panel_pass2");
             break;
     }
     return 0;
 }
-template <int NT, int NS>
+template <int NT, int NS, int WNX>
 int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (c->interleave[which]) {
-        case 0: return panel_launch_nt<NT, 0, NS>(c, which, fixed_block, out, mode);
-        case 1: return panel_launch_nt<NT, 1, NS>(c, which, fixed_block, out, mode);
-        default: return panel_launch_nt<NT, 2, NS>(c, which, fixed_block, out, mode);
+        case 0: return panel_launch_nt<NT, 0, NS, WNX>(c, which, fixed_block, out, mode);
+        case 1: return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
+        default: return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
     }
+}
+template <int NT, int NS>
+int panel_launch_wn(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
+    if constexpr (NT >= 4) {
+        if (c->waves[which] == 4) return panel_launch_ilv<NT, NS, 4>(c, which, fixed_block, out, mode);
+    }
+    return panel_launch_ilv<NT, NS, 0>(c, which, fixed_block, out, mode);
 }
 template <int NS>
 int panel_launch_ns(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (c->k) {
-        case 16: return panel_launch_ilv<1, NS>(c, which, fixed_block, out, mode);
-        case 32: return panel_launch_ilv<2, NS>(c, which, fixed_block, out, mode);
-        case 64: return panel_launch_ilv<4, NS>(c, which, fixed_block, out, mode);
-        default: return panel_launch_ilv<8, NS>(c, which, fixed_block, out, mode);
+        case 16: return panel_launch_wn<1, NS>(c, which, fixed_block, out, mode);
+        case 32: return panel_launch_wn<2, NS>(c, which, fixed_block, out, mode);
+        case 64: return panel_launch_wn<4, NS>(c, which, fixed_block, out, mode);
+        default: return panel_launch_wn<8, NS>(c, which, fixed_block, out, mode);
     }
 }
 int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mode, int ns) {
@@ -423,6 +431,11 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
         if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
+    } else if (!strcmp(key, "waves") || !strcmp(key, "waves1") || !strcmp(key, "waves2")) {
+        if (value != 0 && value != 4) return fail(BPGL_E_ARG, "waves must be 0 (8 waves per block) or 4 (16 waves)");
+        if (value == 4 && c->k < 64) return fail(BPGL_E_ARG, "waves = 4 needs nrhs >= 64");
+        if (key[5] != '2') c->waves[0] = (int)value;
+        if (key[5] != '1') c->waves[1] = (int)value;
     } else if (!strcmp(key, "write_through")) {
         if (value < 0 || value > 15) return fail(BPGL_E_ARG, "write_through is a mask of 4 bits");
         c->wt = (int)value;
@@ -446,6 +459,8 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     if (!strcmp(key, "interleave1")) *value = c->interleave[0];
     else if (!strcmp(key, "interleave2")) *value = c->interleave[1];
     else if (!strcmp(key, "d_split")) *value = c->dsplit;
+    else if (!strcmp(key, "waves1")) *value = c->waves[0];
+    else if (!strcmp(key, "waves2")) *value = c->waves[1];
     else if (!strcmp(key, "write_through")) *value = c->wt;
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
