@@ -124,7 +124,9 @@ def parse():
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
     ap.add_argument("--interleave", type=int, default=-1,
-                    help="panel path mainloop variant 0/1/2 for both passes (-1: library defaults)")
+                    help="panel path mainloop variant 0/1/2/3 for both passes (-1: library defaults)")
+    ap.add_argument("--interleave1", type=int, default=-1, help="panel path pass-1 mainloop variant (-1: default)")
+    ap.add_argument("--interleave2", type=int, default=-1, help="panel path pass-2 mainloop variant (-1: default)")
     ap.add_argument("--d-split", type=int, default=-1, choices=[-1, 1, 2],
                     help="panel path: the direction enters the A D pass as a hi + lo bf16 pair (2) or as its "
                          "bf16 rounding (1); -1: library default")
@@ -132,6 +134,10 @@ def parse():
                     help="panel path, pass 1: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
     ap.add_argument("--waves2", type=int, default=-1, choices=[-1, 0, 4],
                     help="panel path, pass 2: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
+    ap.add_argument("--rows2", type=int, default=-1, choices=[-1, 256, 512],
+                    help="panel path: pass-2 tile rows (512 halves the direction stream; pair with --kchunks 16)")
+    ap.add_argument("--transposed", type=int, default=-1, choices=[-1, 0, 1],
+                    help="panel path: keep a transposed copy of A for the A^T R pass (1) or not (0); -1 default")
     ap.add_argument("--write-through", type=int, default=-1,
                     help="panel path: write-through store sites mask (1 pass-1 epilogue, 2 pass-2 slab, 4 S, "
                          "8 R; -1: library default)")
@@ -478,12 +484,19 @@ def main_panel(args):
     pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks)
     if args.interleave >= 0:
         pl.set_tuning("interleave", args.interleave)
+    for q in (1, 2):
+        if getattr(args, f"interleave{q}") >= 0:
+            pl.set_tuning(f"interleave{q}", getattr(args, f"interleave{q}"))
     if args.d_split > 0:
         pl.set_tuning("d_split", args.d_split)
     if args.defer_x >= 0:
         pl.set_tuning("defer_x", args.defer_x)
     if args.write_through >= 0:
         pl.set_tuning("write_through", args.write_through)
+    if args.rows2 > 0:
+        pl.set_tuning("rows2", args.rows2)
+    if args.transposed >= 0:
+        pl.set_transposed(bool(args.transposed))
     for q in (1, 2):
         if getattr(args, f"waves{q}") >= 0:
             pl.set_tuning(f"waves{q}", getattr(args, f"waves{q}"))
@@ -535,6 +548,7 @@ def main_panel(args):
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
             "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
             "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
+            "transposed_copy": pl._At is not None, "rows2": pl.get_tuning("rows2"),
             "defer_x": pl.get_tuning("defer_x"),
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,

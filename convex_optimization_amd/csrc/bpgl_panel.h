@@ -74,6 +74,8 @@ struct PanelState {
 struct PanelParams {
     const __bf16* A;    // [m][lda]   block b at column offset b * w
     long long lda;
+    const __bf16* At;   // [n][ldat]  optional transposed copy (row j = column j of A) for pass 1, or null
+    long long ldat;
     long long m, w;
     int nblock, k;
     int kchunks;        // pass-2 split of the block's w columns
@@ -419,6 +421,115 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
+// Staggered four-phase form (interleave knob 3; k = 128 with 8 waves: 4 N-tiles per wave).
+// MI355X_MICROARCH.md "Two waves per SIMD": waves w and w + 4 share a SIMD, and in the forms
+// above they run in lockstep -- both read fragments, then both issue MFMAs, so the matrix pipe
+// idles through every read segment.  Here a stage is four phases (h, q): phase (h, 0) reads
+// the A fragments of K-half h and the B fragments of N-tiles 0-1, phase (h, 1) those of
+// N-tiles 2-3; then barrier, 16 MFMAs (4 M-tiles x 2 N-tiles x hi/lo), barrier.  Waves 4-7
+// start one barrier late, so on every SIMD one wave's MFMA segment runs beside its partner's
+// read segment (cdna_hip_programming.md T3/T5: counted vmcnt, raw barriers, setprio around the
+// MFMA cluster).  Stage s's LDS-DMA: O(s+1) and half of A(s+2) in phase 1, the rest of A(s+2)
+// in phase 2 (each slot refilled >= 2 phases after its last read by the later wave group);
+// phase 3 waits until only this wave's A(s+2) pieces are outstanding, so the stage-(s+1) data
+// has landed before the barrier that precedes its first read.
+template <int NT, int PASS, int NS>
+__device__ __forceinline__ void panel_mainloop_stag(char* smem, const __bf16* __restrict__ A, long long lda,
+                                                    long long a_row0, long long a_col0,
+                                                    const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
+                                                    long long ldb, long long b_k0, int nsteps,
+                                                    f32x4 (&acc)[4][PanelGeo<NT, 2, 0>::NTW]) {
+    using G = PanelGeo<NT, NS, 0>;
+    static_assert(G::NTW == 4 && G::NW == 8, "the staggered form is built for 8 waves x 4 N-tiles");
+    static_assert(G::LA % 2 == 0, "A pieces split over two phases");
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    char* abufs = smem;
+    char* obufs = smem + kPanelNA * kPanelAStage;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto piece = [&](int i, int so, int bo, int sa, int ba) {
+        if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
+        if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
+        if (i < G::LO) {
+            panel_op_piece<NT, NS, 0>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
+                                      wave, lane);
+        } else if (PASS == 1) {
+            panel_a1_piece<NT, 0>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+                                  abufs + ba * kPanelAStage, wave, lane);
+        } else {
+            panel_a2_piece<NT, 0>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+                                  abufs + ba * kPanelAStage, wave, lane);
+        }
+    };
+    constexpr int NP = G::LO + G::LA;
+    // prologue: O(0), A(0), A(1); stage 0 landed; then the stagger
+#pragma unroll
+    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
+#pragma unroll
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
+#pragma unroll
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
+    wait_vm_barrier<G::LA>();
+    if (wn == 1) __builtin_amdgcn_s_barrier();   // waves 4-7: one barrier behind (wave-uniform)
+    bf16x8 af[4];
+    int abuf = 0;
+    for (int s = 0; s < nsteps; ++s) {
+        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
+        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
+        const char* ab = abufs + abuf * kPanelAStage;
+        const char* ob = obufs + (s & 1) * G::OStage;
+        static_for<0, 4>([&](auto pc) {
+            constexpr int p = decltype(pc)::value;
+            constexpr int h = p >> 1, q = p & 1;
+            if constexpr (q == 0) {
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt)
+                    af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
+                                       : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
+            }
+            bf16x8 bhi[2], blo[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int rhs = (wn * G::NTW + 2 * q + j) * 16 + (lane & 15);
+                bhi[j] = panel_bfrag(ob, rhs, h, lane);
+                if constexpr (NS == 2) blo[j] = panel_bfrag(ob, G::K + rhs, h, lane);
+            }
+            if constexpr (p == 1) {
+                static_for<0, G::LO + G::LA / 2>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
+            } else if constexpr (p == 2) {
+                static_for<G::LO + G::LA / 2, NP>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
+            } else if constexpr (p == 3) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LA) : "memory");
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[mt][2 * q + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bhi[j], acc[mt][2 * q + j], 0, 0, 0);
+                    if constexpr (NS == 2)
+                        acc[mt][2 * q + j] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], blo[j], acc[mt][2 * q + j], 0, 0, 0);
+                }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        abuf = abuf == 2 ? 0 : abuf + 1;
+    }
+    if (wn == 0) __builtin_amdgcn_s_barrier();   // waves 0-3 take the barrier waves 4-7 took first
+    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
+}
+
 // Write-through (sc1) stores for the bulk outputs a kernel hands to the next launch (split-K
 // slab, D', x, S, R and its split): the lines do not sit dirty in the XCD L2s at the kernel
 // boundary, whose cost grows by ~1 us per 6 MB left dirty (MI355X_MICROARCH.md, "boundary").
@@ -467,7 +578,10 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 // epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
 // per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI, int ILV, int DS, int WNX>
+// AT: A^T is read from the transposed copy p.At with the pass-2 (row-image, ds_read_b128)
+// mainloop instead of transposing LDS reads of A -- the same fragments, the same MFMA order,
+// bitwise the same G.
+template <int NT, int EPI, int ILV, int DS, int WNX, bool AT>
 __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
                                                                          double* __restrict__ Gout) {
     using G = PanelGeo<NT, 2, WNX>;
@@ -478,7 +592,20 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (ILV == 2)
+    if constexpr (AT) {
+        const long long j0 = (long long)mb * p.w + c0;   // first row of A^T
+        if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+            panel_mainloop_stag<NT, 2, 2>(smem, p.At, p.ldat, j0, 0, p.Rh, p.Rl, p.m, 0, (int)(p.m / kPanelK), acc);
+        else if constexpr (ILV >= 2)
+            panel_mainloop_pipe<NT, 2, 2, WNX>(smem, p.At, p.ldat, j0, 0, p.Rh, p.Rl, p.m, 0, (int)(p.m / kPanelK),
+                                               acc);
+        else
+            panel_mainloop<NT, 2, ILV, 2, WNX>(smem, p.At, p.ldat, j0, 0, p.Rh, p.Rl, p.m, 0, (int)(p.m / kPanelK),
+                                               acc);
+    } else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+        panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+                                      (int)(p.m / kPanelK), acc);
+    else if constexpr (ILV >= 2)
         panel_mainloop_pipe<NT, 1, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
                                            (int)(p.m / kPanelK), acc);
     else
@@ -607,7 +734,10 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
     const long long kc = p.w / p.kchunks;
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
-    if constexpr (ILV == 2)
+    if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+        panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
+                                       chunk * kc, (int)(kc / kPanelK), acc);
+    else if constexpr (ILV >= 2)
         panel_mainloop_pipe<NT, 2, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
                                             p.w, chunk * kc, (int)(kc / kPanelK), acc);
     else
@@ -619,6 +749,130 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
         for (int nt = 0; nt < G::NTW; ++nt) {
             const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
             const long long row = r0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
+            wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
+                   make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
+        }
+}
+
+// ---------------------------------------------------------------------------
+// pass 2 on 512-row tiles (tuning knob "rows2" = 512; k = 128).  Every pass-2 block re-reads
+// its column chunk of the k-wide direction panel (hi + lo bf16) from L2 into LDS; with 256-row
+// tiles that stream is as large as the A stream itself (1 GiB per pass at configs[4]).  A
+// 512-row tile halves it and cuts the LDS fragment reads per MFMA by a third: 8 waves of
+// 128 rows x 64 RHS (8 x 4 accumulator tiles), K = 32 per stage (64-byte image rows, XOR
+// swizzled: chunk c of row r at 16 * (c ^ ((r >> 2) & 3)), conflict-free ds_read_b128), both
+// operand streams three stages deep (96 + 48 KiB).  The caller picks kchunks so that
+// (m / 512) x kchunks fills the chip (16 at configs[4]).  Same fp32 accumulation order per
+// output element as the 256-row forms (K ascending, hi before lo): bitwise the same slab.
+// ---------------------------------------------------------------------------
+constexpr int kP2WRows = 512;
+constexpr int kP2WK = 32;
+constexpr int kP2WSlots = 3;
+template <int NS>
+struct P2WGeo {
+    static constexpr int K = 128, T = 512, NW = 8;
+    static constexpr int AStage = kP2WRows * kP2WK * 2;            // 32 KiB
+    static constexpr int OStage = NS * K * kP2WK * 2;              // 16 KiB (NS = 2)
+    static constexpr int LA = AStage / (T * 16);                   // 4 LDS-DMA pieces per thread
+    static constexpr int LO = OStage / (T * 16);                   // 2 (NS = 2), 1 (NS = 1)
+    static constexpr int Smem = kP2WSlots * (AStage + OStage);
+    static_assert(LO >= 1 && Smem <= 160 * 1024, "geometry");
+};
+__device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+template <int NS>
+__global__ __launch_bounds__(512) void k_panel_pass2w(PanelParams p, int fixed_block) {
+    using G = P2WGeo<NS>;
+    __shared__ __attribute__((aligned(16))) char smem[G::Smem];
+    const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    const int nrb = (int)(p.m / kP2WRows);
+    int rb = blockIdx.x % nrb, chunk = blockIdx.x / nrb;
+    if (p.kchunks % 8 == 0) {   // XCD-aware: all row blocks of a column chunk on one XCD (see k_panel_pass2)
+        const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+        chunk = xcd * (p.kchunks / 8) + slot / nrb;
+        rb = slot % nrb;
+    }
+    const long long kc = p.w / p.kchunks;
+    const long long r0 = (long long)rb * kP2WRows;
+    const long long acol = (long long)mb * p.w + chunk * kc;   // first A column of the chunk
+    const long long dcol = chunk * kc;                          // first direction column
+    const int nsteps = (int)(kc / kP2WK);
+    char* abufs = smem;
+    char* obufs = smem + kP2WSlots * G::AStage;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // piece i < LO: direction rows, else A rows; a piece = 16 image rows of 64 B
+    auto piece = [&](int i, int st, int slot) {
+        const long long ks = (long long)st * kP2WK;
+        if (i < G::LO) {
+            const int pc = i * G::NW + wave;
+            const int rr = pc * 16 + (lane >> 2);
+            const int c = swz64(rr, lane & 3);
+            const int hl = rr / G::K, rhs = rr % G::K;
+            glds16o((hl ? p.Dl : p.Dh) + (long long)rhs * p.w + dcol + ks + 8 * c, obufs + slot * G::OStage + pc * 1024);
+        } else {
+            const int pc = (i - G::LO) * G::NW + wave;
+            const int row = pc * 16 + (lane >> 2);
+            const int c = swz64(row, lane & 3);
+            glds16a(p.A + (r0 + row) * p.lda + acol + ks + 8 * c, abufs + slot * G::AStage + pc * 1024);
+        }
+    };
+    constexpr int NP = G::LO + G::LA;
+    // prologue: stages 0 and 1 (each: direction pieces, then A pieces)
+#pragma unroll
+    for (int i = 0; i < NP; ++i) piece(i, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) piece(i, nsteps > 1 ? 1 : 0, 1);
+    int slot = 0;
+    for (int s = 0; s < nsteps; ++s) {
+        // stage s landed (only stage s + 1, the youngest NP operations, may be outstanding);
+        // every wave is past stage s - 1's reads, whose slot (s + 2) % 3 is refilled below
+        wait_vm_barrier<NP>();
+        const int s2 = s + 2 < nsteps ? s + 2 : nsteps - 1;   // clamped tail: loads into an unread slot
+        const int slot2 = slot == 0 ? 2 : slot - 1;
+        const char* ab = abufs + slot * G::AStage;
+        const char* ob = obufs + slot * G::OStage;
+        bf16x8 af[8];
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+            const int row = wm * 128 + mt * 16 + (lane & 15);
+            af[mt] = *reinterpret_cast<const bf16x8*>(ab + row * 64 + 16 * swz64(row, lane >> 4));
+        }
+        static_for<0, 4>([&](auto ntc) {
+            constexpr int nt = decltype(ntc)::value;
+            constexpr int p0 = (nt * NP) / 4, p1 = ((nt + 1) * NP) / 4;   // this group's LDS-DMA pieces
+            static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, s2, slot2); });
+            const int rhs = (wn * 4 + nt) * 16 + (lane & 15);
+            const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(ob + rhs * 64 + 16 * swz64(rhs, lane >> 4));
+            bf16x8 blo;
+            if constexpr (NS == 2) {
+                const int rl = G::K + rhs;
+                blo = *reinterpret_cast<const bf16x8*>(ob + rl * 64 + 16 * swz64(rl, lane >> 4));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bhi, acc[mt][nt], 0, 0, 0);
+                if constexpr (NS == 2)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], blo, acc[mt][nt], 0, 0, 0);
+            }
+            if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x8, 8 * NS, 0);
+        });
+        slot = slot == 2 ? 0 : slot + 1;
+    }
+    wait_vm_barrier<0>();
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const int rhs = (wn * 4 + nt) * 16 + (lane & 15);
+            const long long row = r0 + wm * 128 + mt * 16 + (lane >> 4) * 4;
             wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
                    make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
         }

@@ -112,11 +112,25 @@ def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
     pl = PanelLasso(Ab, 2, nrhs=k, device=0)
     pl.set_tuning("d_split", d_split)
     out = []
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):            # 3: the staggered four-phase form (k = 128; others fall back to 2)
         pl.set_tuning("interleave", v)
         out.append(pl.run(B, mu, 12)["x"])
-    np.testing.assert_array_equal(out[0], out[1])
-    np.testing.assert_array_equal(out[0], out[2])
+    for o in out[1:]:
+        np.testing.assert_array_equal(out[0], o)
+    for w in (0, 4) if k >= 64 else (0,):   # 16 waves per block
+        pl.set_tuning("interleave", 1)
+        pl.set_tuning("waves", w)
+        np.testing.assert_array_equal(pl.run(B, mu, 12)["x"], out[0])
+    pl.set_tuning("waves", 0)
+    pl.set_transposed(True)                 # A^T R from a transposed copy of A
+    for v in (1, 2, 3):
+        pl.set_tuning("interleave", v)
+        np.testing.assert_array_equal(pl.run(B, mu, 12)["x"], out[0])
+    pl.set_transposed(False)
+    if k == 128:                            # pass 2 on 512-row tiles (same chunks: bitwise the same)
+        pl.set_tuning("rows2", 512)
+        np.testing.assert_array_equal(pl.run(B, mu, 12)["x"], out[0])
+        pl.set_tuning("rows2", 256)
     with pytest.raises(Exception):
         pl.set_tuning("no_such_knob", 1)
     with pytest.raises(Exception):
