@@ -134,10 +134,6 @@ def parse():
                     help="panel path, pass 1: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
     ap.add_argument("--waves2", type=int, default=-1, choices=[-1, 0, 4],
                     help="panel path, pass 2: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
-    ap.add_argument("--rows2", type=int, default=-1, choices=[-1, 256, 512],
-                    help="panel path: pass-2 tile rows (512 halves the direction stream; pair with --kchunks 16)")
-    ap.add_argument("--transposed", type=int, default=-1, choices=[-1, 0, 1],
-                    help="panel path: keep a transposed copy of A for the A^T R pass (1) or not (0); -1 default")
     ap.add_argument("--write-through", type=int, default=-1,
                     help="panel path: write-through store sites mask (1 pass-1 epilogue, 2 pass-2 slab, 4 S, "
                          "8 R; -1: library default)")
@@ -493,10 +489,6 @@ def main_panel(args):
         pl.set_tuning("defer_x", args.defer_x)
     if args.write_through >= 0:
         pl.set_tuning("write_through", args.write_through)
-    if args.rows2 > 0:
-        pl.set_tuning("rows2", args.rows2)
-    if args.transposed >= 0:
-        pl.set_transposed(bool(args.transposed))
     for q in (1, 2):
         if getattr(args, f"waves{q}") >= 0:
             pl.set_tuning(f"waves{q}", getattr(args, f"waves{q}"))
@@ -548,7 +540,6 @@ def main_panel(args):
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
             "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
             "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
-            "transposed_copy": pl._At is not None, "rows2": pl.get_tuning("rows2"),
             "defer_x": pl.get_tuning("defer_x"),
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,

@@ -74,8 +74,6 @@ struct PanelState {
 struct PanelParams {
     const __bf16* A;    // [m][lda]   block b at column offset b * w
     long long lda;
-    const __bf16* At;   // [n][ldat]  optional transposed copy (row j = column j of A) for pass 1, or null
-    long long ldat;
     long long m, w;
     int nblock, k;
     int kchunks;        // pass-2 split of the block's w columns
@@ -578,10 +576,7 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 // epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
 // per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-// AT: A^T is read from the transposed copy p.At with the pass-2 (row-image, ds_read_b128)
-// mainloop instead of transposing LDS reads of A -- the same fragments, the same MFMA order,
-// bitwise the same G.
-template <int NT, int EPI, int ILV, int DS, int WNX, bool AT>
+template <int NT, int EPI, int ILV, int DS, int WNX>
 __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
                                                                          double* __restrict__ Gout) {
     using G = PanelGeo<NT, 2, WNX>;
@@ -592,17 +587,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (AT) {
-        const long long j0 = (long long)mb * p.w + c0;   // first row of A^T
-        if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
-            panel_mainloop_stag<NT, 2, 2>(smem, p.At, p.ldat, j0, 0, p.Rh, p.Rl, p.m, 0, (int)(p.m / kPanelK), acc);
-        else if constexpr (ILV >= 2)
-            panel_mainloop_pipe<NT, 2, 2, WNX>(smem, p.At, p.ldat, j0, 0, p.Rh, p.Rl, p.m, 0, (int)(p.m / kPanelK),
-                                               acc);
-        else
-            panel_mainloop<NT, 2, ILV, 2, WNX>(smem, p.At, p.ldat, j0, 0, p.Rh, p.Rl, p.m, 0, (int)(p.m / kPanelK),
-                                               acc);
-    } else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+    if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
                                       (int)(p.m / kPanelK), acc);
     else if constexpr (ILV >= 2)
@@ -749,130 +734,6 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
         for (int nt = 0; nt < G::NTW; ++nt) {
             const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
             const long long row = r0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
-            wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
-                   make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
-        }
-}
-
-// ---------------------------------------------------------------------------
-// pass 2 on 512-row tiles (tuning knob "rows2" = 512; k = 128).  Every pass-2 block re-reads
-// its column chunk of the k-wide direction panel (hi + lo bf16) from L2 into LDS; with 256-row
-// tiles that stream is as large as the A stream itself (1 GiB per pass at configs[4]).  A
-// 512-row tile halves it and cuts the LDS fragment reads per MFMA by a third: 8 waves of
-// 128 rows x 64 RHS (8 x 4 accumulator tiles), K = 32 per stage (64-byte image rows, XOR
-// swizzled: chunk c of row r at 16 * (c ^ ((r >> 2) & 3)), conflict-free ds_read_b128), both
-// operand streams three stages deep (96 + 48 KiB).  The caller picks kchunks so that
-// (m / 512) x kchunks fills the chip (16 at configs[4]).  Same fp32 accumulation order per
-// output element as the 256-row forms (K ascending, hi before lo): bitwise the same slab.
-// ---------------------------------------------------------------------------
-constexpr int kP2WRows = 512;
-constexpr int kP2WK = 32;
-constexpr int kP2WSlots = 3;
-template <int NS>
-struct P2WGeo {
-    static constexpr int K = 128, T = 512, NW = 8;
-    static constexpr int AStage = kP2WRows * kP2WK * 2;            // 32 KiB
-    static constexpr int OStage = NS * K * kP2WK * 2;              // 16 KiB (NS = 2)
-    static constexpr int LA = AStage / (T * 16);                   // 4 LDS-DMA pieces per thread
-    static constexpr int LO = OStage / (T * 16);                   // 2 (NS = 2), 1 (NS = 1)
-    static constexpr int Smem = kP2WSlots * (AStage + OStage);
-    static_assert(LO >= 1 && Smem <= 160 * 1024, "geometry");
-};
-__device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); }
-
-template <int NS>
-__global__ __launch_bounds__(512) void k_panel_pass2w(PanelParams p, int fixed_block) {
-    using G = P2WGeo<NS>;
-    __shared__ __attribute__((aligned(16))) char smem[G::Smem];
-    const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    const int nrb = (int)(p.m / kP2WRows);
-    int rb = blockIdx.x % nrb, chunk = blockIdx.x / nrb;
-    if (p.kchunks % 8 == 0) {   // XCD-aware: all row blocks of a column chunk on one XCD (see k_panel_pass2)
-        const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-        chunk = xcd * (p.kchunks / 8) + slot / nrb;
-        rb = slot % nrb;
-    }
-    const long long kc = p.w / p.kchunks;
-    const long long r0 = (long long)rb * kP2WRows;
-    const long long acol = (long long)mb * p.w + chunk * kc;   // first A column of the chunk
-    const long long dcol = chunk * kc;                          // first direction column
-    const int nsteps = (int)(kc / kP2WK);
-    char* abufs = smem;
-    char* obufs = smem + kP2WSlots * G::AStage;
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // piece i < LO: direction rows, else A rows; a piece = 16 image rows of 64 B
-    auto piece = [&](int i, int st, int slot) {
-        const long long ks = (long long)st * kP2WK;
-        if (i < G::LO) {
-            const int pc = i * G::NW + wave;
-            const int rr = pc * 16 + (lane >> 2);
-            const int c = swz64(rr, lane & 3);
-            const int hl = rr / G::K, rhs = rr % G::K;
-            glds16o((hl ? p.Dl : p.Dh) + (long long)rhs * p.w + dcol + ks + 8 * c, obufs + slot * G::OStage + pc * 1024);
-        } else {
-            const int pc = (i - G::LO) * G::NW + wave;
-            const int row = pc * 16 + (lane >> 2);
-            const int c = swz64(row, lane & 3);
-            glds16a(p.A + (r0 + row) * p.lda + acol + ks + 8 * c, abufs + slot * G::AStage + pc * 1024);
-        }
-    };
-    constexpr int NP = G::LO + G::LA;
-    // prologue: stages 0 and 1 (each: direction pieces, then A pieces)
-#pragma unroll
-    for (int i = 0; i < NP; ++i) piece(i, 0, 0);
-#pragma unroll
-    for (int i = 0; i < NP; ++i) piece(i, nsteps > 1 ? 1 : 0, 1);
-    int slot = 0;
-    for (int s = 0; s < nsteps; ++s) {
-        // stage s landed (only stage s + 1, the youngest NP operations, may be outstanding);
-        // every wave is past stage s - 1's reads, whose slot (s + 2) % 3 is refilled below
-        wait_vm_barrier<NP>();
-        const int s2 = s + 2 < nsteps ? s + 2 : nsteps - 1;   // clamped tail: loads into an unread slot
-        const int slot2 = slot == 0 ? 2 : slot - 1;
-        const char* ab = abufs + slot * G::AStage;
-        const char* ob = obufs + slot * G::OStage;
-        bf16x8 af[8];
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-            const int row = wm * 128 + mt * 16 + (lane & 15);
-            af[mt] = *reinterpret_cast<const bf16x8*>(ab + row * 64 + 16 * swz64(row, lane >> 4));
-        }
-        static_for<0, 4>([&](auto ntc) {
-            constexpr int nt = decltype(ntc)::value;
-            constexpr int p0 = (nt * NP) / 4, p1 = ((nt + 1) * NP) / 4;   // this group's LDS-DMA pieces
-            static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, s2, slot2); });
-            const int rhs = (wn * 4 + nt) * 16 + (lane & 15);
-            const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(ob + rhs * 64 + 16 * swz64(rhs, lane >> 4));
-            bf16x8 blo;
-            if constexpr (NS == 2) {
-                const int rl = G::K + rhs;
-                blo = *reinterpret_cast<const bf16x8*>(ob + rl * 64 + 16 * swz64(rl, lane >> 4));
-            }
-#pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bhi, acc[mt][nt], 0, 0, 0);
-                if constexpr (NS == 2)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], blo, acc[mt][nt], 0, 0, 0);
-            }
-            if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
-            __builtin_amdgcn_sched_group_barrier(0x8, 8 * NS, 0);
-        });
-        slot = slot == 2 ? 0 : slot + 1;
-    }
-    wait_vm_barrier<0>();
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const int rhs = (wn * 4 + nt) * 16 + (lane & 15);
-            const long long row = r0 + wm * 128 + mt * 16 + (lane >> 4) * 4;
             wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
                    make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
         }

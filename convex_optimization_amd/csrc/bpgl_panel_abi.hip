@@ -34,7 +34,6 @@ struct bpgl_panel {
     bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
     int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
     int waves[2] = {0, 0};        // waves along the RHS per pass: 0 = 2 (8 waves), 4 = 16 waves ("waves" knobs)
-    int rows2 = 256;              // pass-2 tile rows ("rows2" knob: 256 or 512)
     int dsplit = 2;               // bf16 pieces of the solver's direction (d_split knob)
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
@@ -78,28 +77,13 @@ template <int NT, int ILV, int NS, int WNX>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
         case 0:
-            if (c->p.At) {
-                if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX, true>), dim3((unsigned)(c->w / kPanelRows)),
-                                             dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
-                else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX, true>), dim3((unsigned)(c->w / kPanelRows)),
-                                        dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
-            } else {
-                if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX, false>), dim3((unsigned)(c->w / kPanelRows)),
-                                             dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
-                else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX, false>), dim3((unsigned)(c->w / kPanelRows)),
-                                        dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
-            }
+            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX>), dim3((unsigned)(c->w / kPanelRows)),
+                                         dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX>), dim3((unsigned)(c->w / kPanelRows)),
+                                    dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
             LAUNCH_CHECK("k_panel_pass1");
             break;
         case 1:
-            if constexpr (NT == 8) {
-                if (c->rows2 == 512) {
-                    hipLaunchKernelGGL((k_panel_pass2w<NS>), dim3((unsigned)((c->m / kP2WRows) * c->kchunks)), dim3(512),
-                                       0, c->stream, c->p, fixed_block);
-                    LAUNCH_CHECK("k_panel_pass2w");
-                    break;
-                }
-            }
             hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS, WNX>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
                                dim3(PanelGeo<NT, NS, WNX>::T), 0, c->stream, c->p, fixed_block);
             LAUNCH_CHECK("k_panel_pass2");
@@ -252,18 +236,6 @@ void bpgl_panel_destroy(bpgl_panel* c) {
 }
 
 int64_t bpgl_panel_scratch_bytes(const bpgl_panel* c) { return c ? panel_layout(c).total : -1; }
-
-int bpgl_panel_bind_transposed(bpgl_panel* c, const void* At, int64_t ldat) {
-    if (!c) return fail(BPGL_E_ARG, "null panel context");
-    if (!c->bound) return fail(BPGL_E_STATE, "bpgl_panel_bind must come first");
-    if (At && ((uintptr_t)At) % 16) return fail(BPGL_E_ARG, "At must be 16-byte aligned");
-    if (At && (ldat < c->m || ldat % 8)) return fail(BPGL_E_ARG, "ldat must be >= m and a multiple of 8");
-    c->p.At = (const __bf16*)At;
-    c->p.ldat = At ? ldat : 0;
-    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-    c->solver = false;   // the captured iteration launches the other pass-1 kernel
-    return 0;
-}
 
 int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, int64_t scratch_bytes) {
     if (!c) return fail(BPGL_E_ARG, "null panel context");
@@ -467,11 +439,6 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
         if (value == 4 && c->k < 64) return fail(BPGL_E_ARG, "waves = 4 needs nrhs >= 64");
         if (key[5] != '2') c->waves[0] = (int)value;
         if (key[5] != '1') c->waves[1] = (int)value;
-    } else if (!strcmp(key, "rows2")) {
-        if (value != 256 && value != 512) return fail(BPGL_E_ARG, "rows2 must be 256 or 512");
-        if (value == 512 && (c->k != 128 || c->m % kP2WRows || (c->w / c->kchunks) % kP2WK))
-            return fail(BPGL_E_ARG, "rows2 = 512 needs nrhs = 128, m a multiple of 512 and w / kchunks a multiple of 32");
-        c->rows2 = (int)value;
     } else if (!strcmp(key, "write_through")) {
         if (value < 0 || value > 15) return fail(BPGL_E_ARG, "write_through is a mask of 4 bits");
         c->wt = (int)value;
@@ -496,7 +463,6 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "interleave2")) *value = c->interleave[1];
     else if (!strcmp(key, "d_split")) *value = c->dsplit;
     else if (!strcmp(key, "waves1")) *value = c->waves[0];
-    else if (!strcmp(key, "rows2")) *value = c->rows2;
     else if (!strcmp(key, "waves2")) *value = c->waves[1];
     else if (!strcmp(key, "write_through")) *value = c->wt;
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;

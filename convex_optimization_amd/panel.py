@@ -33,7 +33,6 @@ _PANEL_SIGS = {
     "bpgl_panel_scratch_bytes": (_i64, [_p]),
     "bpgl_panel_bind": (ctypes.c_int, [_p, _p, _i64, _p, _i64]),
     "bpgl_panel_diag": (ctypes.c_int, [_p, _p]),
-    "bpgl_panel_bind_transposed": (ctypes.c_int, [_p, _p, _i64]),
     "bpgl_panel_mtm": (ctypes.c_int, [_p, _i32, _p, _p]),
     "bpgl_panel_mm": (ctypes.c_int, [_p, _i32, _p, _p]),
     "bpgl_panel_reset": (ctypes.c_int, [_p, _p, _p, _p, _i64, ctypes.c_int]),
@@ -62,7 +61,7 @@ class PanelLasso:
 
     KERNEL_KINDS = ("pass1_mfma", "pass2_mfma", "reduce", "step", "update")
 
-    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0, transposed=False):
+    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0):
         L = _lib()
         self.Block = int(Block)
         self.nrhs = int(nrhs)
@@ -90,9 +89,6 @@ class PanelLasso:
                     "bpgl_panel_bind")
             self._diag = torch.empty(K, dtype=torch.float64, device=self.device)
             N.check(L.bpgl_panel_diag(ctx, N.ptr(self._diag)), "bpgl_panel_diag")
-            self._At = None
-            if transposed:
-                self.set_transposed(True)
         self.stream.synchronize()
         kc = ctypes.c_int32()
         N.check(L.bpgl_panel_geometry(ctx, ctypes.byref(kc)), "bpgl_panel_geometry")
@@ -114,17 +110,6 @@ class PanelLasso:
         with torch.cuda.stream(self.stream):
             yield
         cur.wait_stream(self.stream)
-
-    def set_transposed(self, on):
-        """Keep a transposed bf16 copy of A (n x m, +n*m*2 bytes of HBM) for the A^T R pass, which then
-        reads it like the A D pass reads A (include/bpgl.h bpgl_panel_bind_transposed); bitwise the same."""
-        with self._on_stream():
-            if on and self._At is None:
-                self._At = self._A.t().contiguous()
-            elif not on:
-                self._At = None
-            N.check(_lib().bpgl_panel_bind_transposed(self._ctx, N.ptr(self._At), self.MAT_HEIGHT if on else 0),
-                    "bpgl_panel_bind_transposed")
 
     @property
     def A_bf16(self):

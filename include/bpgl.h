@@ -272,10 +272,6 @@ int64_t bpgl_panel_scratch_bytes(const bpgl_panel* ctx);
 int bpgl_panel_bind(bpgl_panel* ctx, const void* A /* [m][lda] bf16 */, int64_t lda, void* scratch,
                     int64_t scratch_bytes);
 int bpgl_panel_diag(bpgl_panel* ctx, double* out /* nullable, n fp64 */);
-/* Optional transposed copy of A (At [n][ldat] bf16, row j = column j of A, caller-owned; NULL
- * drops it): pass 1 (A^T R) then reads At with the row-image mainloop of pass 2 instead of
- * transposing LDS reads of A.  Bitwise the same results; A stays bound for pass 2. */
-int bpgl_panel_bind_transposed(bpgl_panel* ctx, const void* At, int64_t ldat);
 /* G = A_b^T R  and  S = A_b D  (fp64 in/out, device; split-bf16 MFMA inside) */
 int bpgl_panel_mtm(bpgl_panel* ctx, int32_t block, const double* R, double* G);
 int bpgl_panel_mm(bpgl_panel* ctx, int32_t block, const double* D, double* S);
