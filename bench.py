@@ -137,6 +137,9 @@ def parse():
     ap.add_argument("--write-through", type=int, default=-1,
                     help="panel path: write-through store sites mask (1 pass-1 epilogue, 2 pass-2 slab, 4 S, "
                          "8 R; -1: library default)")
+    ap.add_argument("--op-pad", type=int, default=0,
+                    help="panel path: bf16 elements appended to each RHS row of the operand images (multiple of 64)")
+    ap.add_argument("--lda-pad", type=int, default=0, help="panel path: columns appended to each row of bf16 A")
     ap.add_argument("--defer-x", type=int, default=-1, choices=[-1, 0, 1],
                     help="panel path, one block: apply x += gamma D in the next pass-1 epilogue (1) or in the "
                          "update kernel (0); -1: library default")
@@ -477,7 +480,7 @@ def main_panel(args):
     A = torch.randn(m, n, device="cuda", generator=g)
     A /= A.norm(dim=1, keepdim=True)
     Xt = torch.randn(n, k, device="cuda", generator=g) * (torch.rand(n, k, device="cuda", generator=g) < 0.4)
-    pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks)
+    pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks, op_pad=args.op_pad, lda_pad=args.lda_pad)
     if args.interleave >= 0:
         pl.set_tuning("interleave", args.interleave)
     for q in (1, 2):
@@ -540,7 +543,7 @@ def main_panel(args):
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
             "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
             "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
-            "defer_x": pl.get_tuning("defer_x"),
+            "defer_x": pl.get_tuning("defer_x"), "op_pad": pl.get_tuning("op_pad"), "lda_pad": args.lda_pad,
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
             "iter_roofline_frac": iters_s * alg_iter / (HBM_PEAK_GBS * 1e9),

@@ -77,9 +77,10 @@ struct PanelParams {
     long long m, w;
     int nblock, k;
     int kchunks;        // pass-2 split of the block's w columns
-    __bf16* Rh;         // [k][m]
+    long long ldr, ldd; // leading dimensions of the bf16 operand images (m, w + the "op_pad" knob)
+    __bf16* Rh;         // [k][ldr]
     __bf16* Rl;
-    __bf16* Dh;         // [k][w]
+    __bf16* Dh;         // [k][ldd]
     __bf16* Dl;
     float* X;           // [nblock][k][w]
     double* Ax;         // [nblock][k][m]
@@ -588,13 +589,13 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
     if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
-        panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+        panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                       (int)(p.m / kPanelK), acc);
     else if constexpr (ILV >= 2)
-        panel_mainloop_pipe<NT, 1, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+        panel_mainloop_pipe<NT, 1, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                            (int)(p.m / kPanelK), acc);
     else
-        panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.m, 0,
+        panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                            (int)(p.m / kPanelK), acc);
 
     // C layout: row = (lane>>4)*4 + r (A column), col = lane & 15 (RHS)
@@ -629,9 +630,9 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
             const float4 x4 = *reinterpret_cast<const float4*>(xp);
             float xs[4] = {x4.x, x4.y, x4.z, x4.w};
             if (fx) {
-                const bf16x4 ph = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.w + j);
+                const bf16x4 ph = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.ldd + j);
                 bf16x4 pl;
-                if constexpr (DS == 2) pl = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.w + j);
+                if constexpr (DS == 2) pl = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.ldd + j);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     double dq = (double)(float)ph[r];
@@ -661,9 +662,9 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
                 const double e = fabs(g - proj(g - x, -mu, mu));
                 err = (e > err || e != e) ? e : err;
             }
-            wt_put(p.wt & 1, p.Dh, (long long)p.k * p.w, (long long)rhs * p.w + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
+            wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
             if constexpr (DS == 2)
-                wt_put(p.wt & 1, p.Dl, (long long)p.k * p.w, (long long)rhs * p.w + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
+                wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
         }
         // lanes l, l^16, l^32, l^48 share the RHS
         sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
@@ -720,14 +721,14 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
     if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
-        panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.w,
+        panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);
     else if constexpr (ILV >= 2)
         panel_mainloop_pipe<NT, 2, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
-                                            p.w, chunk * kc, (int)(kc / kPanelK), acc);
+                                            p.ldd, chunk * kc, (int)(kc / kPanelK), acc);
     else
         panel_mainloop<NT, 2, ILV, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
-                                            p.w, chunk * kc, (int)(kc / kPanelK), acc);
+                                            p.ldd, chunk * kc, (int)(kc / kPanelK), acc);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -890,10 +891,12 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
     for (unsigned u = blockIdx.x * kThreads + threadIdx.x; u < nu; u += gridDim.x * kThreads) {
         if (u < ux) {
             const long long e = 8ll * u;
-            const double g = p.gamma[u / w8];
-            const bf16x8v dh = *reinterpret_cast<const bf16x8v*>(p.Dh + e);
+            const unsigned rhs = u / w8;
+            const long long de = (long long)rhs * p.ldd + (e - (long long)rhs * p.w);   // operand image index
+            const double g = p.gamma[rhs];
+            const bf16x8v dh = *reinterpret_cast<const bf16x8v*>(p.Dh + de);
             bf16x8v dl;
-            if constexpr (DS == 2) dl = *reinterpret_cast<const bf16x8v*>(p.Dl + e);
+            if constexpr (DS == 2) dl = *reinterpret_cast<const bf16x8v*>(p.Dl + de);
             float* xp = p.X + (long long)mb * nx + e;
             float4 x0 = *reinterpret_cast<const float4*>(xp);
             float4 x1 = *reinterpret_cast<const float4*>(xp + 4);
@@ -910,7 +913,9 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
         else {
             const unsigned v = u - ux;
             const long long e = 4ll * v;
-            const double g = p.gamma[v / m4];
+            const unsigned rhs = v / m4;
+            const long long re = (long long)rhs * p.ldr + (e - (long long)rhs * p.m);   // operand image index
+            const double g = p.gamma[rhs];
             double r[4];
             __bf16 hi[4], lo[4];
             if constexpr (NB1) {
@@ -942,8 +947,8 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
             }
             wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
             wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
-            wt_put(p.wt & 8, p.Rh, nr, e, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
-            wt_put(p.wt & 8, p.Rl, nr, e, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+            wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+            wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, false);
@@ -958,7 +963,9 @@ __global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p) {
     typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
     for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
         const long long e = 4ll * v;
-        const double g = p.gamma[v / m4];
+        const unsigned rhs = v / m4;
+        const long long re = (long long)rhs * p.ldr + (e - (long long)rhs * p.m);   // operand image index
+        const double g = p.gamma[rhs];
         const double2 r01 = *reinterpret_cast<const double2*>(p.R + e);
         const double2 r23 = *reinterpret_cast<const double2*>(p.R + e + 2);
         const double2 s01 = *reinterpret_cast<const double2*>(p.S + e);
@@ -969,8 +976,8 @@ __global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p) {
         for (int q = 0; q < 4; ++q) split_bf16(r[q], hi[q], lo[q]);
         wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
         wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
-        wt_put(p.wt & 8, p.Rh, nr, e, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
-        wt_put(p.wt & 8, p.Rl, nr, e, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+        wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+        wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, true);
 }
@@ -985,10 +992,12 @@ __global__ __launch_bounds__(kThreads) void k_panel_flush(PanelParams p) {
     const unsigned w8 = (unsigned)(p.w / 8);
     for (unsigned u = blockIdx.x * kThreads + threadIdx.x; u < (unsigned)(nx / 8); u += gridDim.x * kThreads) {
         const long long e = 8ll * u;
-        const double g = p.gamma[u / w8];
-        const bf16x8v dh = *reinterpret_cast<const bf16x8v*>(p.Dh + e);
+        const unsigned rhs = u / w8;
+        const long long de = (long long)rhs * p.ldd + (e - (long long)rhs * p.w);   // operand image index
+        const double g = p.gamma[rhs];
+        const bf16x8v dh = *reinterpret_cast<const bf16x8v*>(p.Dh + de);
         bf16x8v dl;
-        if constexpr (DS == 2) dl = *reinterpret_cast<const bf16x8v*>(p.Dl + e);
+        if constexpr (DS == 2) dl = *reinterpret_cast<const bf16x8v*>(p.Dl + de);
         float* xp = p.X + e;
         float4 x0 = *reinterpret_cast<const float4*>(xp);
         float4 x1 = *reinterpret_cast<const float4*>(xp + 4);
@@ -1007,14 +1016,17 @@ __global__ void k_panel_clear_pending(PanelParams p) {
     if (threadIdx.x == 0) p.st->pending = 0;
 }
 
-// split an fp64 [k][len] operand into hi/lo bf16; optionally R = -B (reset)
-__global__ __launch_bounds__(kThreads) void k_panel_split(const double* __restrict__ src, long long n,
-                                                          __bf16* __restrict__ hi, __bf16* __restrict__ lo,
-                                                          double sign, double* __restrict__ copy) {
+// split an fp64 [k][len] operand into hi/lo bf16 images [k][ld]; optionally R = -B (reset)
+__global__ __launch_bounds__(kThreads) void k_panel_split(const double* __restrict__ src, long long n, long long len,
+                                                          long long ld, __bf16* __restrict__ hi,
+                                                          __bf16* __restrict__ lo, double sign,
+                                                          double* __restrict__ copy) {
     for (long long e = (long long)blockIdx.x * kThreads + threadIdx.x; e < n; e += (long long)gridDim.x * kThreads) {
         const double v = sign * src[e];
         if (copy) copy[e] = v;
-        split_bf16(v, hi[e], lo[e]);
+        const long long row = e / len;
+        const long long d = row * ld + (e - row * len);
+        split_bf16(v, hi[d], lo[d]);
     }
 }
 

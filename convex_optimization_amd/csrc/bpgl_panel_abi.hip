@@ -37,6 +37,9 @@ struct bpgl_panel {
     int dsplit = 2;               // bf16 pieces of the solver's direction (d_split knob)
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
+    int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
+    int64_t ldr() const { return m + op_pad; }
+    int64_t ldd() const { return w + op_pad; }
 };
 
 namespace {
@@ -49,10 +52,10 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     PanelLayout L;
     const int64_t km = (int64_t)c->k * c->m, kw = (int64_t)c->k * c->w;
     L.st = k.take(sizeof(PanelState));
-    L.Rh = k.take(2 * km);
-    L.Rl = k.take(2 * km);
-    L.Dh = k.take(2 * kw);
-    L.Dl = k.take(2 * kw);
+    L.Rh = k.take(2 * (int64_t)c->k * c->ldr());
+    L.Rl = k.take(2 * (int64_t)c->k * c->ldr());
+    L.Dh = k.take(2 * (int64_t)c->k * c->ldd());
+    L.Dl = k.take(2 * (int64_t)c->k * c->ldd());
     L.X = k.take(4 * kw * c->nblock);
     L.Ax = k.take(8 * km * c->nblock);
     L.B = k.take(8 * km);
@@ -170,9 +173,12 @@ int panel_iteration(bpgl_panel* c, int64_t it) {
     panel_ev(c, it, 4, 1);
     return 0;
 }
-int panel_split(bpgl_panel* c, const double* src, int64_t n, __bf16* hi, __bf16* lo, double sign, double* copy) {
+// src [k][len] fp64 -> hi/lo images [k][ld]
+int panel_split(bpgl_panel* c, const double* src, int64_t len, int64_t ld, __bf16* hi, __bf16* lo, double sign,
+                double* copy) {
+    const int64_t n = (int64_t)c->k * len;
     hipLaunchKernelGGL(k_panel_split, dim3((unsigned)std::min<int64_t>(cdiv(n, kThreads), 2048)), dim3(kThreads), 0,
-                       c->stream, src, n, hi, lo, sign, copy);
+                       c->stream, src, n, len, ld, hi, lo, sign, copy);
     LAUNCH_CHECK("k_panel_split");
     return 0;
 }
@@ -256,6 +262,8 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.nblock = c->nblock;
     p.k = c->k;
     p.kchunks = c->kchunks;
+    p.ldr = c->ldr();
+    p.ldd = c->ldd();
     p.st = (PanelState*)(s + L.st);
     p.Rh = (__bf16*)(s + L.Rh);
     p.Rl = (__bf16*)(s + L.Rl);
@@ -303,7 +311,7 @@ int bpgl_panel_mtm(bpgl_panel* c, int32_t block, const double* R, double* G) {
     if (block < 0 || block >= c->nblock) return fail(BPGL_E_ARG, "block out of range");
     if (!R || !G) return fail(BPGL_E_ARG, "null operand");
     HIP_TRY(hipSetDevice(c->device));
-    if ((rc = panel_split(c, R, (int64_t)c->k * c->m, c->p.Rh, c->p.Rl, 1.0, nullptr))) return rc;
+    if ((rc = panel_split(c, R, c->m, c->ldr(), c->p.Rh, c->p.Rl, 1.0, nullptr))) return rc;
     c->solver = false;   // Rh/Rl now hold the caller's operand
     return panel_launch(c, 0, block, G, 0, 2);
 }
@@ -314,7 +322,7 @@ int bpgl_panel_mm(bpgl_panel* c, int32_t block, const double* D, double* S) {
     if (block < 0 || block >= c->nblock) return fail(BPGL_E_ARG, "block out of range");
     if (!D || !S) return fail(BPGL_E_ARG, "null operand");
     HIP_TRY(hipSetDevice(c->device));
-    if ((rc = panel_split(c, D, (int64_t)c->k * c->w, c->p.Dh, c->p.Dl, 1.0, nullptr))) return rc;
+    if ((rc = panel_split(c, D, c->w, c->ldd(), c->p.Dh, c->p.Dl, 1.0, nullptr))) return rc;
     c->solver = false;
     if ((rc = panel_launch(c, 1, block, nullptr, 0, 2))) return rc;
     return panel_reduce(c, S, 0);
@@ -334,7 +342,7 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     HIP_TRY(hipMemsetAsync(p.X, 0, 4 * (int64_t)c->k * c->w * c->nblock, c->stream));
     HIP_TRY(hipMemsetAsync(p.Ax, 0, 8 * km * c->nblock, c->stream));
     // x = 0 => Ax = 0, R = -B
-    if ((rc = panel_split(c, p.B, km, p.Rh, p.Rl, -1.0, p.R))) return rc;
+    if ((rc = panel_split(c, p.B, c->m, c->ldr(), p.Rh, p.Rl, -1.0, p.R))) return rc;
     p.err_iter = err_iter;
     p.rec_len = err_iter ? record_len : 0;
     hipLaunchKernelGGL(k_panel_reset_state, dim3(1), dim3(64), 0, c->stream, c->p);
@@ -450,6 +458,14 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;
+    } else if (!strcmp(key, "op_pad")) {   // changes the scratch layout: only before bpgl_panel_bind
+        if (c->bound) return fail(BPGL_E_STATE, "op_pad must be set before bpgl_panel_bind");
+        if (value < 0 || value % 64 || value > 4096)
+            return fail(BPGL_E_ARG, "op_pad must be a multiple of 64 in [0, 4096] (bf16 elements)");
+        if ((int64_t)c->k * (c->w + value) >= (1ll << 31) || (int64_t)c->k * (c->m + value) >= (1ll << 31))
+            return fail(BPGL_E_ARG, "nrhs * (width + op_pad) must stay below 2^31");
+        c->op_pad = value;
+        return 0;
     } else {
         return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     }
@@ -466,6 +482,7 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "waves2")) *value = c->waves[1];
     else if (!strcmp(key, "write_through")) *value = c->wt;
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
+    else if (!strcmp(key, "op_pad")) *value = c->op_pad;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;
 }

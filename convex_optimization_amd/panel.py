@@ -61,7 +61,10 @@ class PanelLasso:
 
     KERNEL_KINDS = ("pass1_mfma", "pass2_mfma", "reduce", "step", "update")
 
-    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0):
+    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0, op_pad=0, lda_pad=0):
+        """op_pad: bf16 elements appended to each right-hand side's row of the residual / direction
+        images (a multiple of 64; layout only, bitwise-identical results).  lda_pad: columns appended to
+        each row of the stored bf16 A (a multiple of 8; the padding is never read)."""
         L = _lib()
         self.Block = int(Block)
         self.nrhs = int(nrhs)
@@ -78,14 +81,22 @@ class PanelLasso:
         N.check(L.bpgl_panel_create(ctypes.byref(ctx), self.device.index, H, K, self.Block, self.nrhs,
                                     int(kchunks), ctypes.c_void_p(self.stream.cuda_stream)), "bpgl_panel_create")
         self._ctx = ctx
+        if op_pad:
+            N.check(L.bpgl_panel_set_tuning(ctx, b"op_pad", int(op_pad)), "bpgl_panel_set_tuning(op_pad)")
+        lda = K + int(lda_pad)
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             A_src = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))
-            self._A = A_src.to(device=self.device, dtype=torch.bfloat16).contiguous()     # [m][n]
+            if lda_pad:
+                self._A_store = torch.zeros((H, lda), dtype=torch.bfloat16, device=self.device)
+                self._A_store[:, :K].copy_(A_src.to(device=self.device, dtype=torch.bfloat16))
+                self._A = self._A_store[:, :K]                                                 # [m][n], row pitch lda
+            else:
+                self._A = A_src.to(device=self.device, dtype=torch.bfloat16).contiguous()     # [m][n]
             nbytes = int(L.bpgl_panel_scratch_bytes(ctx))
             self._scratch = torch.empty(nbytes // 8 + 64, dtype=torch.float64, device=self.device)
             base = (self._scratch.data_ptr() + 255) // 256 * 256
-            N.check(L.bpgl_panel_bind(ctx, ctypes.c_void_p(self._A.data_ptr()), K, ctypes.c_void_p(base), nbytes),
+            N.check(L.bpgl_panel_bind(ctx, ctypes.c_void_p(self._A.data_ptr()), lda, ctypes.c_void_p(base), nbytes),
                     "bpgl_panel_bind")
             self._diag = torch.empty(K, dtype=torch.float64, device=self.device)
             N.check(L.bpgl_panel_diag(ctx, N.ptr(self._diag)), "bpgl_panel_diag")

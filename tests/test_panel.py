@@ -128,6 +128,30 @@ def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
         pl.set_tuning("d_split", 3)
 
 
+@pytest.mark.parametrize("blocks,d_split", [(1, 2), (2, 2), (2, 1)])
+def test_panel_padded_layouts_are_bitwise_neutral(blocks, d_split):
+    """op_pad (row pitch of the residual / direction images) and lda_pad (row pitch of the stored A)
+    change addresses only: solver iterates, products and the API GEMMs are bitwise identical."""
+    Ab, B, mu = instance(512, 2048, 64, seed=21)
+    ref = PanelLasso(Ab, blocks, nrhs=64, device=0)
+    ref.set_tuning("d_split", d_split)
+    x0 = ref.run(B, mu, 14)["x"]
+    R = np.random.RandomState(2).randn(512, 64)
+    D = np.random.RandomState(3).randn(2048 // blocks, 64)
+    G0, S0 = ref.mat_tMulMat(R, blocks - 1).cpu().numpy(), ref.matMulMat(D, 0).cpu().numpy()
+    for op_pad, lda_pad in ((64, 0), (0, 64), (192, 8)):
+        pl = PanelLasso(Ab, blocks, nrhs=64, device=0, op_pad=op_pad, lda_pad=lda_pad)
+        assert pl.get_tuning("op_pad") == op_pad
+        pl.set_tuning("d_split", d_split)
+        np.testing.assert_array_equal(pl.run(B, mu, 14)["x"], x0)
+        np.testing.assert_array_equal(pl.mat_tMulMat(R, blocks - 1).cpu().numpy(), G0)
+        np.testing.assert_array_equal(pl.matMulMat(D, 0).cpu().numpy(), S0)
+        with pytest.raises(Exception):
+            pl.set_tuning("op_pad", 0)     # layout knob: only before bind
+    with pytest.raises(Exception):
+        PanelLasso(Ab, blocks, nrhs=64, device=0, op_pad=32)   # not a multiple of 64
+
+
 @pytest.mark.parametrize("kchunks", [1, 2, 4, 16])
 def test_panel_split_k_chunks_agree(kchunks):
     """Pass-2 column chunks only change the fp64 summation order of the fp32 chunk partials."""
