@@ -139,8 +139,6 @@ def parse():
                          "8 R; -1: library default)")
     ap.add_argument("--op-pad", type=int, default=0,
                     help="panel path: bf16 elements appended to each RHS row of the operand images (multiple of 64)")
-    ap.add_argument("--a-transposed", type=int, default=0, choices=[0, 1],
-                    help="panel path: keep a transposed copy of A for pass 1's register-ring form (interleave1 4)")
     ap.add_argument("--lda-pad", type=int, default=0, help="panel path: columns appended to each row of bf16 A")
     ap.add_argument("--defer-x", type=int, default=-1, choices=[-1, 0, 1],
                     help="panel path, one block: apply x += gamma D in the next pass-1 epilogue (1) or in the "
@@ -482,8 +480,7 @@ def main_panel(args):
     A = torch.randn(m, n, device="cuda", generator=g)
     A /= A.norm(dim=1, keepdim=True)
     Xt = torch.randn(n, k, device="cuda", generator=g) * (torch.rand(n, k, device="cuda", generator=g) < 0.4)
-    pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks, op_pad=args.op_pad, lda_pad=args.lda_pad,
-                    a_transposed=args.a_transposed)
+    pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks, op_pad=args.op_pad, lda_pad=args.lda_pad)
     if args.interleave >= 0:
         pl.set_tuning("interleave", args.interleave)
     for q in (1, 2):
@@ -547,7 +544,6 @@ def main_panel(args):
             "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
             "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
             "defer_x": pl.get_tuning("defer_x"), "op_pad": pl.get_tuning("op_pad"), "lda_pad": args.lda_pad,
-            "a_transposed": pl.get_tuning("a_transposed"),
             "interleave12": [pl.get_tuning("interleave1"), pl.get_tuning("interleave2")],
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,

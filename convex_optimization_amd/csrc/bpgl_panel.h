@@ -74,8 +74,6 @@ struct PanelState {
 struct PanelParams {
     const __bf16* A;    // [m][lda]   block b at column offset b * w
     long long lda;
-    const __bf16* At;   // [n][ldt]   transposed copy of A (the "a_transposed" knob; pass 1's register-ring form)
-    long long ldt;
     long long m, w;
     int nblock, k;
     int kchunks;        // pass-2 split of the block's w columns
@@ -126,8 +124,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 // float -> bf16, round to nearest even.  The float is made opaque first: otherwise the compiler may
 // fold (bf16)(float)d into one double -> bf16 rounding in some kernels and not in others, and the
-// two differ where (float)d lands on a bf16 tie (a pass-1 form once split one direction element
-// differently from the others that way).
+// two differ where (float)d lands on a bf16 tie (a register-ring pass-1 variant, measured and
+// removed, once split one direction element differently from the LDS-DMA form that way).
 __device__ __forceinline__ __bf16 to_bf16(float v) {
     asm volatile("" : "+v"(v));
     return (__bf16)v;
@@ -581,7 +579,7 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
     lo = to_bf16((float)(v - (double)(float)hi));
 }
 
-// pass-1 epilogue (shared by the LDS-DMA forms and the register-ring form): EPI 0 writes G
+// pass-1 epilogue: EPI 0 writes G
 // [k][w] fp64 (API); EPI 1 is the fused shrink -- the direction D' in DS bf16 pieces, the norms
 // per RHS and block.  The wave owns output rows c0 + 64 wm .. (A columns) x RHS tiles wn * NTW ..;
 // T threads per block; smem holds at least 4 * k * 3 doubles and is free (after a barrier).
@@ -760,196 +758,6 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
             wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
                    make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
         }
-}
-
-// ---------------------------------------------------------------------------
-// pass 2, register-ring form (interleave2 = 4).  The LDS-DMA forms above move every A byte
-// and every operand byte through the CU's LDS-DMA path, which caps a pass near 35 GB/s per CU
-// (A + operand bytes; profiles/r02/sweeps/panel_ksweep.json).  Here the A fragments go HBM ->
-// VGPRs directly (a DR-deep register ring of 16-B non-temporal loads in MFMA fragment shape,
-// no LDS), and only the k-wide operand is staged in LDS (two images, filled by register
-// staging: loaded two stages ahead, written one stage ahead; one barrier per stage).
-// 4 waves, one per SIMD; wave w owns rows r0 + 64w .. + 63 (4 M-tiles) x all k RHS.  The
-// per-element MFMA chain runs in the same order as the forms above (stage, K half, hi, lo),
-// so the results are bitwise identical.  Every load of a stage is compiler-counted (plain
-// loads, no LDS-DMA beside them): the operand loads of a stage are issued before its A
-// loads, so the wait before an operand write never covers the younger A stages.
-// ---------------------------------------------------------------------------
-typedef unsigned int pu32x4v __attribute__((ext_vector_type(4)));
-template <int NT, int NS>
-struct RGeo {
-    static constexpr int K = 16 * NT;                        // right-hand sides
-    static constexpr int OStage = NS * K * kPanelK * 2;      // operand image bytes per stage
-    static constexpr int OPL = OStage / (256 * 16);          // 16-B operand pieces per lane per stage
-    static constexpr int Smem = 2 * OStage;
-    static constexpr bool ok = OPL >= 1 && OStage % (256 * 16) == 0;   // the stage covers the 4 waves
-};
-// acc[mt][nt] += X[xrow0 + 16 mt + i][K] . (Oh [+ Ol])[nt * 16 + j][ocol + K] over nsteps stages of 64:
-// xrow = this lane's fragment row pointer (row xrow0 + (lane & 15), column K0 + 8 (lane >> 4)), x16 = 16
-// rows of X; the operand images [k][ld] bf16 at column ocol.
-template <int NT, int NS, int DR>
-__device__ __forceinline__ void panel_rmainloop(char* smem, const __bf16* __restrict__ xrow, long long x16,
-                                                const __bf16* __restrict__ oh, const __bf16* __restrict__ ol,
-                                                long long ld, long long ocol, int nsteps, f32x4 (&acc)[4][NT]) {
-    using G = RGeo<NT, NS>;
-    static_assert(G::ok, "operand stage must cover every lane");
-    constexpr int K = G::K, OStage = G::OStage, OPL = G::OPL;
-    constexpr int UNR = DR % 2 ? 2 * DR : DR;   // ring slots and image parity static
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // operand piece i of this lane: image row rr (hl = rr / K, rhs = rr % K), chunk lane & 7
-    int odst[OPL];
-    const __bf16* osrc[OPL];
-#pragma unroll
-    for (int i = 0; i < OPL; ++i) {
-        const int rr = (i * 4 + wave) * 8 + (lane >> 3);
-        const int hl = rr / K, rhs = rr % K;
-        odst[i] = rr * 128 + 16 * swz128(rr, lane & 7);
-        osrc[i] = (hl ? ol : oh) + (long long)rhs * ld + ocol + 8 * (lane & 7);
-    }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    pu32x4v ar[DR][4][2];
-    pu32x4v ost[2][OPL];
-    auto loadA = [&](int s, int slot) {
-        const long long off = 64ll * (s < nsteps ? s : nsteps - 1);   // clamped tail: harmless re-reads
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                ar[slot][mt][h] =
-                    __builtin_nontemporal_load(reinterpret_cast<const pu32x4v*>(xrow + mt * x16 + off + 32 * h));
-    };
-    auto loadO = [&](int s, int set) {
-        const long long off = 64ll * (s < nsteps ? s : nsteps - 1);
-#pragma unroll
-        for (int i = 0; i < OPL; ++i) ost[set][i] = *reinterpret_cast<const pu32x4v*>(osrc[i] + off);
-    };
-    auto writeO = [&](int set, int buf) {
-#pragma unroll
-        for (int i = 0; i < OPL; ++i) *reinterpret_cast<pu32x4v*>(smem + buf * OStage + odst[i]) = ost[set][i];
-    };
-    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-
-    // prologue: O(0) -> image 0; O(1) staged; A(0) .. A(DR-2) in flight
-    loadO(0, 0);
-#pragma unroll
-    for (int s = 0; s + 1 < DR; ++s) loadA(s, s);
-    loadO(1, 1);
-    writeO(0, 0);
-    barrier();
-    // one stage; GUARD: the remainder copy of the loop (nsteps not a multiple of UNR)
-    auto stage = [&](auto GUARD, auto qc, int base) {
-        constexpr int q = decltype(qc)::value;
-        const int s = base + q;
-        if (decltype(GUARD)::value && s >= nsteps) return;   // block-uniform
-        loadO(s + 2, q & 1);                         // set q & 1 held O(s), written at stage s - 1
-        loadA(s + DR - 1, (q + DR - 1) % DR);        // slot of A(s - 1), consumed at stage s - 1
-        __builtin_amdgcn_sched_barrier(0);           // keep the loads at the head of the stage
-        const char* ob = smem + (q & 1) * OStage;
-        static_for<0, 2>([&](auto hc) {
-            constexpr int h = decltype(hc)::value;
-            static_for<0, NT>([&](auto ntc) {
-                constexpr int nt = decltype(ntc)::value;
-                const int rhs = nt * 16 + (lane & 15);
-                const bf16x8 b_hi = panel_bfrag(ob, rhs, h, lane);
-                bf16x8 b_lo;
-                if constexpr (NS == 2) b_lo = panel_bfrag(ob, K + rhs, h, lane);
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
-                    const bf16x8 af = __builtin_bit_cast(bf16x8, ar[q % DR][mt][h]);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b_hi, acc[mt][nt], 0, 0, 0);
-                    if constexpr (NS == 2)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b_lo, acc[mt][nt], 0, 0, 0);
-                }
-            });
-        });
-        __builtin_amdgcn_sched_barrier(0);
-        writeO((q + 1) & 1, (q + 1) & 1);            // O(s + 1) into the image read at stage s - 1
-        barrier();
-    };
-    using G0 = std::integral_constant<bool, false>;
-    using G1 = std::integral_constant<bool, true>;
-    int base = 0;
-    for (; base + UNR <= nsteps; base += UNR) static_for<0, UNR>([&](auto qc) { stage(G0{}, qc, base); });
-    for (; base < nsteps; base += UNR) static_for<0, UNR>([&](auto qc) { stage(G1{}, qc, base); });
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads have landed
-}
-
-template <int NT, int NS, int DR>
-__global__ __launch_bounds__(256, 1) void k_panel_rpass2(PanelParams p, int fixed_block) {
-    using G = RGeo<NT, NS>;
-    __shared__ __attribute__((aligned(16))) char smem[G::Smem];
-    const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nrb = (int)(p.m / kPanelRows);
-    int rb = blockIdx.x % nrb, chunk = blockIdx.x / nrb;   // same XCD-aware map as k_panel_pass2
-    if (p.kchunks % 8 == 0) {
-        const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-        chunk = xcd * (p.kchunks / 8) + slot / nrb;
-        rb = slot % nrb;
-    } else if (8 % p.kchunks == 0 && nrb % (8 / p.kchunks) == 0) {
-        const int xpc = 8 / p.kchunks, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-        chunk = xcd / xpc;
-        rb = (xcd % xpc) * (nrb / xpc) + slot;
-    }
-    const long long kc = p.w / p.kchunks;
-    const long long rw = (long long)rb * kPanelRows + wave * 64;     // this wave's first row
-    const long long ocol = (long long)chunk * kc;                    // first operand column
-    const __bf16* xrow = p.A + (rw + (lane & 15)) * p.lda + (long long)mb * p.w + ocol + 8 * (lane >> 4);
-    f32x4 acc[4][NT];
-    panel_rmainloop<NT, NS, DR>(smem, xrow, 16 * p.lda, p.Dh, p.Dl, p.ldd, ocol, (int)(kc / kPanelK), acc);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            const int rhs = nt * 16 + (lane & 15);
-            const long long row = rw + mt * 16 + (lane >> 4) * 4;
-            wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
-                   make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
-        }
-}
-
-// pass 1, register-ring form (interleave1 = 4): G = A_m^T R from the transposed copy At, whose
-// rows (columns of A) are contiguous along K = the rows of A, so the A^T fragments stream
-// HBM -> VGPRs like pass 2's; the residual hi + lo through the LDS image.  grid = w / 256.
-template <int NT, int EPI, int DS, int DR>
-__global__ __launch_bounds__(256, 1) void k_panel_rpass1(PanelParams p, int fixed_block, double* __restrict__ Gout) {
-    using G = RGeo<NT, 2>;
-    constexpr int SM = G::Smem > 4 * G::K * 3 * 8 ? G::Smem : 4 * G::K * 3 * 8;
-    __shared__ __attribute__((aligned(16))) char smem[SM];
-    const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
-    const __bf16* xrow = p.At + ((long long)mb * p.w + c0 + wave * 64 + (lane & 15)) * p.ldt + 8 * (lane >> 4);
-    f32x4 acc[4][NT];
-    panel_rmainloop<NT, 2, DR>(smem, xrow, 16 * p.ldt, p.Rh, p.Rl, p.ldr, 0, (int)(p.m / kPanelK), acc);
-    panel_pass1_epilogue<NT, EPI, DS>(p, mb, c0, wave, 0, 256, acc, smem, Gout);
-}
-
-// At[j][i] = A[i][j]: 64 x 64 tiles through LDS (16-B loads and stores).  grid = (n / 64, m / 64)
-__global__ __launch_bounds__(256) void k_panel_transpose(const __bf16* __restrict__ A, long long lda,
-                                                         __bf16* __restrict__ At, long long ldt) {
-    __shared__ __bf16 tile[64][64 + 8];
-    const long long j0 = (long long)blockIdx.x * 64, i0 = (long long)blockIdx.y * 64;
-    for (int c = threadIdx.x; c < 512; c += 256) {          // 64 rows x 8 chunks of 8
-        const int r = c >> 3, q = c & 7;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(A + (i0 + r) * lda + j0 + 8 * q);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) tile[r][8 * q + e] = v[e];
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < 512; c += 256) {          // 64 columns x 8 chunks of 8 rows
-        const int j = c >> 3, q = c & 7;
-        bf16x8 v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = tile[8 * q + e][j];
-        *reinterpret_cast<bf16x8*>(At + (j0 + j) * ldt + i0 + 8 * q) = v;
-    }
 }
 
 __device__ __forceinline__ void panel_st_sc1(double* q, double v) {

@@ -19,9 +19,7 @@ using namespace bpgl_host;
 // panel path (k right-hand sides, bf16 A, MFMA): BASELINE configs[4]
 // ===========================================================================
 constexpr int kPanelKinds = 5;
-#ifndef BPGL_RPASS_DR
-#define BPGL_RPASS_DR 4   // A register-ring depth of k_panel_rpass2 (stages)
-#endif   // pass1, pass2, reduce, step, update
+   // pass1, pass2, reduce, step, update
 
 struct bpgl_panel {
     int device = 0;
@@ -41,7 +39,6 @@ struct bpgl_panel {
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
-    int a_transposed = 0;         // keep a transposed copy of A in the scratch for pass 1's register-ring form (before bind)
     int64_t ldr() const { return m + op_pad; }
     int64_t ldd() const { return w + op_pad; }
 };
@@ -49,7 +46,7 @@ struct bpgl_panel {
 namespace {
 
 struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, At, total;
+    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -74,7 +71,6 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.gamma = k.take(8 * c->k);
     L.err_rhs = k.take(8 * c->k);
     L.cnt = k.take(8 * c->k);
-    L.At = c->a_transposed ? k.take(2 * c->n * c->m) : 0;   // [n][m] bf16
     L.total = k.off;
     return L;
 }
@@ -85,28 +81,15 @@ template <int NT, int ILV, int NS, int WNX>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
         case 0:
-            if constexpr (ILV == 4) {   // register-ring form on the transposed copy
-                if (mode) hipLaunchKernelGGL((k_panel_rpass1<NT, 1, NS, BPGL_RPASS_DR>), dim3((unsigned)(c->w / kPanelRows)),
-                                             dim3(256), 0, c->stream, c->p, fixed_block, out);
-                else hipLaunchKernelGGL((k_panel_rpass1<NT, 0, 2, BPGL_RPASS_DR>), dim3((unsigned)(c->w / kPanelRows)),
-                                        dim3(256), 0, c->stream, c->p, fixed_block, out);
-            } else {
-                if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX>), dim3((unsigned)(c->w / kPanelRows)),
-                                             dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
-                else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX>), dim3((unsigned)(c->w / kPanelRows)),
-                                        dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
-            }
+            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX>), dim3((unsigned)(c->w / kPanelRows)),
+                                         dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX>), dim3((unsigned)(c->w / kPanelRows)),
+                                    dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
             LAUNCH_CHECK("k_panel_pass1");
             break;
         case 1:
-            if constexpr (ILV == 4) {   // register-ring form (the operand stage must cover the 4 waves)
-                hipLaunchKernelGGL((k_panel_rpass2<NT, NS, BPGL_RPASS_DR>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
-                                   dim3(256), 0, c->stream, c->p, fixed_block);
-            } else {
-                hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS, WNX>),
-                                   dim3((unsigned)((c->m / kPanelRows) * c->kchunks)), dim3(PanelGeo<NT, NS, WNX>::T),
-                                   0, c->stream, c->p, fixed_block);
-            }
+            hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS, WNX>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
+                               dim3(PanelGeo<NT, NS, WNX>::T), 0, c->stream, c->p, fixed_block);
             LAUNCH_CHECK("k_panel_pass2");
             break;
     }
@@ -118,10 +101,6 @@ int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int
         case 0: return panel_launch_nt<NT, 0, NS, WNX>(c, which, fixed_block, out, mode);
         case 1: return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
         case 2: return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
-        case 4:   // register-ring forms: pass 2 always, pass 1 on the transposed copy of A
-            if constexpr (WNX == 0 && RGeo<NT, NS>::ok && RGeo<NT, 2>::ok)
-                if (which == 1 || c->a_transposed) return panel_launch_nt<NT, 4, NS, WNX>(c, which, fixed_block, out, mode);
-            return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
         default:
             if constexpr (NT == 8 && WNX == 0) return panel_launch_nt<NT, 3, NS, WNX>(c, which, fixed_block, out, mode);
             else return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
@@ -305,16 +284,9 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.gamma = (double*)(s + L.gamma);
     p.err_rhs = (double*)(s + L.err_rhs);
     p.cnt = (unsigned long long*)(s + L.cnt);
-    p.At = c->a_transposed ? (const __bf16*)(s + L.At) : nullptr;
-    p.ldt = c->m;
     p.wt = c->wt;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(s, 0, L.At ? L.At : L.total, c->stream));
-    if (c->a_transposed) {   // the transposed copy, once per bind (A is read-only to the library)
-        hipLaunchKernelGGL(k_panel_transpose, dim3((unsigned)(c->n / 64), (unsigned)(c->m / 64)), dim3(256), 0,
-                           c->stream, p.A, lda, const_cast<__bf16*>(p.At), p.ldt);
-        LAUNCH_CHECK("k_panel_transpose");
-    }
+    HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
     c->bound = true;
     c->have_diag = false;
     c->solver = false;
@@ -468,7 +440,7 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     if (!c || !key) return fail(BPGL_E_ARG, "null argument");
     const bool both = !strcmp(key, "interleave");
     if (both || !strcmp(key, "interleave1") || !strcmp(key, "interleave2")) {
-        if (value < 0 || value > 4) return fail(BPGL_E_ARG, "interleave must be 0 ... 4");
+        if (value < 0 || value > 3) return fail(BPGL_E_ARG, "interleave must be 0, 1, 2 or 3");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
     } else if (!strcmp(key, "waves") || !strcmp(key, "waves1") || !strcmp(key, "waves2")) {
@@ -487,11 +459,6 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;
-    } else if (!strcmp(key, "a_transposed")) {   // changes the scratch layout: only before bpgl_panel_bind
-        if (c->bound) return fail(BPGL_E_STATE, "a_transposed must be set before bpgl_panel_bind");
-        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "a_transposed must be 0 or 1");
-        c->a_transposed = (int)value;
-        return 0;
     } else if (!strcmp(key, "op_pad")) {   // changes the scratch layout: only before bpgl_panel_bind
         if (c->bound) return fail(BPGL_E_STATE, "op_pad must be set before bpgl_panel_bind");
         if (value < 0 || value % 64 || value > 4096)
@@ -517,7 +484,6 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "write_through")) *value = c->wt;
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else if (!strcmp(key, "op_pad")) *value = c->op_pad;
-    else if (!strcmp(key, "a_transposed")) *value = c->a_transposed;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;
 }

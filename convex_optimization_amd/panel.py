@@ -61,11 +61,10 @@ class PanelLasso:
 
     KERNEL_KINDS = ("pass1_mfma", "pass2_mfma", "reduce", "step", "update")
 
-    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0, op_pad=0, lda_pad=0, a_transposed=0):
+    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0, op_pad=0, lda_pad=0):
         """op_pad: bf16 elements appended to each right-hand side's row of the residual / direction
         images (a multiple of 64; layout only, bitwise-identical results).  lda_pad: columns appended to
-        each row of the stored bf16 A (a multiple of 8; the padding is never read).  a_transposed: keep a
-        transposed copy of A in the scratch (+2 m n bytes) for pass 1's register-ring form (interleave1 = 4)."""
+        each row of the stored bf16 A (a multiple of 8; the padding is never read)."""
         L = _lib()
         self.Block = int(Block)
         self.nrhs = int(nrhs)
@@ -84,8 +83,6 @@ class PanelLasso:
         self._ctx = ctx
         if op_pad:
             N.check(L.bpgl_panel_set_tuning(ctx, b"op_pad", int(op_pad)), "bpgl_panel_set_tuning(op_pad)")
-        if a_transposed:
-            N.check(L.bpgl_panel_set_tuning(ctx, b"a_transposed", 1), "bpgl_panel_set_tuning(a_transposed)")
         lda = K + int(lda_pad)
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):

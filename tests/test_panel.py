@@ -112,20 +112,11 @@ def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
     pl = PanelLasso(Ab, 2, nrhs=k, device=0)
     pl.set_tuning("d_split", d_split)
     out = []
-    for v in (0, 1, 2, 3, 4):         # 3: the staggered four-phase form (k = 128; others fall back to 2);
-        #                               4: pass 2 on the register-ring kernel (pass 1 falls back to 2)
+    for v in (0, 1, 2, 3):            # 3: the staggered four-phase form (k = 128; others fall back to 2)
         pl.set_tuning("interleave", v)
         out.append(pl.run(B, mu, 12)["x"])
     for o in out[1:]:
         np.testing.assert_array_equal(out[0], o)
-    # both passes on the register-ring kernels (pass 1 reads the transposed copy of A)
-    pt = PanelLasso(Ab, 2, nrhs=k, device=0, a_transposed=1)
-    assert pt.get_tuning("a_transposed") == 1
-    pt.set_tuning("d_split", d_split)
-    pt.set_tuning("interleave", 4)
-    np.testing.assert_array_equal(pt.run(B, mu, 12)["x"], out[0])
-    R = np.random.RandomState(4).randn(512, k)
-    np.testing.assert_array_equal(pt.mat_tMulMat(R, 1).cpu().numpy(), pl.mat_tMulMat(R, 1).cpu().numpy())
     for w in (0, 4) if k >= 64 else (0,):   # 16 waves per block
         pl.set_tuning("interleave", 1)
         pl.set_tuning("waves", w)
