@@ -1,0 +1,77 @@
+"""Two RCCL ranks exchanging through libbpgl's own communicator (column shards: the reference's
+P-way split, cpu_calculation.py:23-27 / lasso.py:101-126; row shards: one feature block).
+
+Both ranks run on the one GPU of the test box as two processes under torch.distributed.run,
+each announcing its own NCCL_HOSTID so RCCL accepts them (the all-reduce then crosses loopback
+sockets instead of xGMI: correctness only, no timing).  Unlike tests/test_rowshard.py, whose
+multi-rank cases sum the exchange buffers in the test, here the product's ncclAllReduce (inside
+the captured graph and eager) is the exchange.  Row shards on a shared GPU cannot keep the
+one-pass kernel's blocks co-resident, so they normally finish on the two-pass row iteration
+ -- also the product path.  Tolerance: the reference fixture's x within
+1e-9 relative l2 (as every solver test), the ranks' x bit-identical (rows), graph = eager.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(case, shard, tmp_path, world=2):
+    env = dict(os.environ)
+    env.pop("NCCL_HOSTID", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "rccl_ranks_worker.py"), case, shard, str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    return [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
+
+
+def rel(a, b):
+    a, b = np.asarray(a).reshape(-1), np.asarray(b).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("case", ["c1_b2_p4_f32in", "bound_b4_p2_f32in"])
+def test_two_rccl_ranks_column_shards(golden, case, tmp_path):
+    from convex_optimization_amd import distributed as D
+    fx = golden(case)
+    out = _launch(case, "columns", tmp_path)
+    for tag in ("graph", "eager"):
+        x = D.assemble_x([o[f"x_{tag}"] for o in out], int(fx["BLOCK"]))
+        assert rel(x, fx["x"]) <= 1e-9, (tag, rel(x, fx["x"]))
+        for o in out:
+            assert int(o[f"t_last_{tag}"]) == int(fx["t_last"]) and bool(o[f"stopped_{tag}"]) == bool(fx["stopped"])
+        T = int(fx["t_last"]) + 1
+        np.testing.assert_allclose(out[0][f"err_{tag}"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
+        np.testing.assert_array_equal(out[0][f"err_{tag}"][:T], out[1][f"err_{tag}"][:T])
+    np.testing.assert_array_equal(out[0]["x_graph"], out[0]["x_eager"])
+
+
+def test_two_rccl_ranks_row_shards(golden, tmp_path):
+    fx = golden("c1_b1_p1_f32in")
+    out = _launch("c1_b1_p1_f32in", "rows", tmp_path)
+    np.testing.assert_array_equal(out[0]["diag"], out[1]["diag"])      # all-reduced column norms
+    np.testing.assert_allclose(out[0]["diag"], fx["d_ATA"].reshape(-1), rtol=1e-12)
+    for tag in ("graph", "eager"):
+        np.testing.assert_array_equal(out[0][f"x_{tag}"], out[1][f"x_{tag}"])   # x replicated bit for bit
+        assert rel(out[0][f"x_{tag}"], fx["x"]) <= 1e-9, (tag, rel(out[0][f"x_{tag}"], fx["x"]))
+        T = int(fx["ITER_MAX"])
+        np.testing.assert_allclose(out[0][f"err_{tag}"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
+    print("row-shard fallbacks per rank:", [int(o["fallbacks"]) for o in out])

@@ -4,9 +4,10 @@ local A once and all-reduces [U | r.s23 | s23.s23] (w_pad + 2 fp64).
 
 The reference has no row split (it shards columns, cpu_calculation.py:23-27); the iteration
 it computes is the same (lasso.py:102-157), so parity is against the reference's fixtures and
-the single-rank solver.  Several ranks cannot share one GPU under RCCL, so the multi-rank
-cases here run the ranks' kernels on one GPU with the exchange done by the test (phases 0/1
-per iteration, 2/3 for the exact-gradient refresh); the RCCL leg runs with one rank.
+the single-rank solver.  The multi-rank cases here run the ranks' kernels in one process on
+one GPU with the exchange done by the test (phases 0/1 per iteration, 2/3 for the exact-gradient
+refresh); the RCCL leg runs with one rank here and with two processes (each its own NCCL host id,
+loopback sockets) in tests/test_rccl_ranks.py.
 Tolerances (relative l2 on x): reference fixtures <= 1e-9 (as every solver test); rank
 counts against each other and against the single-rank one-pass path <= 1e-10 (the sums over
 ranks change the fp64 summation order only)."""
