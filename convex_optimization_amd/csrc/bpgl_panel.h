@@ -427,120 +427,6 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
-// Register-staged form (interleave knob 4): the same LDS images, filled by plain 16-B loads into
-// VGPRs and ds_write_b128 instead of LDS-DMA.  At k = 128 the DMA forms move 64 KiB per stage and
-// CU through global_load_lds, whose fill rate (one 1-KiB piece per ~60 cycles per CU with the
-// MFMA loop's LDS reads beside it) bounds the pass; here the bytes travel
-// HBM/L2 -> VGPR -> LDS.  Each wave holds two stages of pieces in registers (loaded two stages
-// ahead, written to the idle image at the end of the stage before their use); images: A and the
-// k-wide operand, two each; one barrier per stage.  Same fragment reads and MFMA order as the
-// forms above: bitwise identical results.
-typedef unsigned int pu32x4v __attribute__((ext_vector_type(4)));
-template <int NT, int PASS, int NS, int WNX>
-__device__ __forceinline__ void panel_mainloop_rs(char* smem, const __bf16* __restrict__ A, long long lda,
-                                                  long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
-                                                  const __bf16* __restrict__ bl, long long ldb, long long b_k0,
-                                                  int nsteps, f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
-    using G = PanelGeo<NT, NS, WNX>;
-    constexpr int NPA = G::LA, NPO = G::LO;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    char* abufs = smem;                           // 2 x kPanelAStage
-    char* obufs = smem + 2 * kPanelAStage;        // 2 x OStage
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // piece sources (the DMA forms' swizzled source addresses) at stage 0; destinations lane-linear
-    const __bf16* asrc[NPA];
-    const __bf16* osrc[NPO];
-    bool oval[NPO];
-#pragma unroll
-    for (int i = 0; i < NPA; ++i) {
-        const int pc = i * G::NW + wave;
-        if constexpr (PASS == 1) {
-            const int row = pc * 2 + (lane >> 5);
-            asrc[i] = A + (a_row0 + row) * lda + a_col0 + 8 * swz512(row, lane & 31);
-        } else {
-            const int row = pc * 8 + (lane >> 3);
-            asrc[i] = A + (a_row0 + row) * lda + a_col0 + 8 * swz128(row, lane & 7);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NPO; ++i) {
-        const int pc = i * G::NW + wave;
-        oval[i] = pc * 8 < NS * G::K;   // wave-uniform
-        const int rr = oval[i] ? pc * 8 + (lane >> 3) : 0;
-        const int hl = rr / G::K, rhs = rr % G::K;
-        osrc[i] = (hl ? bl : bh) + (long long)rhs * ldb + b_k0 + 8 * swz128(rr, lane & 7);
-    }
-    const long long astep = PASS == 1 ? kPanelK * lda : kPanelK;   // one stage of K
-    pu32x4v ra[2][NPA], ro[2][NPO];
-    auto load = [&](int s, int set) {
-        const long long sc = s < nsteps ? s : nsteps - 1;   // clamped tail: harmless re-reads
-#pragma unroll
-        for (int i = 0; i < NPA; ++i)
-            ra[set][i] = __builtin_nontemporal_load(reinterpret_cast<const pu32x4v*>(asrc[i] + sc * astep));
-#pragma unroll
-        for (int i = 0; i < NPO; ++i)
-            if (oval[i]) ro[set][i] = *reinterpret_cast<const pu32x4v*>(osrc[i] + sc * kPanelK);
-    };
-    auto write = [&](int set, int buf) {
-#pragma unroll
-        for (int i = 0; i < NPA; ++i)
-            *reinterpret_cast<pu32x4v*>(abufs + buf * kPanelAStage + (i * G::NW + wave) * 1024 + 16 * lane) = ra[set][i];
-#pragma unroll
-        for (int i = 0; i < NPO; ++i)
-            if (oval[i])
-                *reinterpret_cast<pu32x4v*>(obufs + buf * G::OStage + (i * G::NW + wave) * 1024 + 16 * lane) = ro[set][i];
-    };
-    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-    load(0, 0);
-    load(1, 1);
-    write(0, 0);
-    barrier();
-    auto stage = [&](auto GUARD, auto qc, int base) {
-        constexpr int q = decltype(qc)::value;
-        const int s = base + q;
-        if (decltype(GUARD)::value && s >= nsteps) return;   // block-uniform
-        load(s + 2, q);                                        // set q held stage s, written at stage s - 1
-        __builtin_amdgcn_sched_barrier(0);
-        const char* ab = abufs + q * kPanelAStage;
-        const char* ob = obufs + q * G::OStage;
-        static_for<0, 2>([&](auto hc) {
-            constexpr int h = decltype(hc)::value;
-            bf16x8 af[4];
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-                af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
-                                   : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
-            static_for<0, G::NTW>([&](auto ntc) {
-                constexpr int nt = decltype(ntc)::value;
-                const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
-                const bf16x8 b_hi = panel_bfrag(ob, rhs, h, lane);
-                bf16x8 b_lo;
-                if constexpr (NS == 2) b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    if constexpr (NS == 2)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
-                }
-            });
-        });
-        __builtin_amdgcn_sched_barrier(0);
-        write(q ^ 1, q ^ 1);                                   // stage s + 1 into the image read at stage s - 1
-        barrier();
-    };
-    using G0 = std::integral_constant<bool, false>;
-    using G1 = std::integral_constant<bool, true>;
-    int base = 0;
-    for (; base + 2 <= nsteps; base += 2) static_for<0, 2>([&](auto qc) { stage(G0{}, qc, base); });
-    for (; base < nsteps; base += 2) static_for<0, 2>([&](auto qc) { stage(G1{}, qc, base); });
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads have landed
-}
-
 // Staggered four-phase form (interleave knob 3; k = 128 with 8 waves: 4 N-tiles per wave).
 // MI355X_MICROARCH.md "Two waves per SIMD": waves w and w + 4 share a SIMD, and in the forms
 // above they run in lockstep -- both read fragments, then both issue MFMAs, so the matrix pipe
@@ -813,10 +699,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (ILV == 4)
-        panel_mainloop_rs<NT, 1, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
-                                         (int)(p.m / kPanelK), acc);
-    else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+    if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                       (int)(p.m / kPanelK), acc);
     else if constexpr (ILV >= 2)
@@ -857,10 +740,7 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
     const long long kc = p.w / p.kchunks;
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
-    if constexpr (ILV == 4)
-        panel_mainloop_rs<NT, 2, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
-                                          chunk * kc, (int)(kc / kPanelK), acc);
-    else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+    if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);
     else if constexpr (ILV >= 2)
