@@ -386,6 +386,18 @@ def cpu_baseline(gc, b, mu, seconds, cores, cpu_info, share_note=""):
     out["numpy_fp64"] = {"value": n_np / (time.perf_counter() - t0), "unit": "iters/s",
                          "threads": "OpenBLAS default (OMP_NUM_THREADS=" + os.environ.get("OMP_NUM_THREADS", "unset") + ")",
                          "sample": f"oracle.run_numpy, {n_np} iterations from x=0 on the same A (as fp64)"}
+    # and the fp32-storage variant (the reference's TYPE='float' CPU path: sgemv on fp32 A, fp64 elsewhere)
+    del A64
+    t0 = time.perf_counter()
+    oracle.run_numpy(A, bh, mu, gc.Block, 1, gemv_f32=True)
+    per = time.perf_counter() - t0
+    n_np = int(max(2, min(100, seconds / 3 / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    oracle.run_numpy(A, bh, mu, gc.Block, n_np, gemv_f32=True)
+    out["numpy_fp32_storage"] = {"value": n_np / (time.perf_counter() - t0), "unit": "iters/s",
+                                 "threads": out["numpy_fp64"]["threads"],
+                                 "sample": f"oracle.run_numpy(gemv_f32=True), {n_np} iterations from x=0 on the "
+                                           "same fp32 A (fp32 GEMVs, fp64 vectors)"}
     return out
 
 

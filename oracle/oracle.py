@@ -117,12 +117,15 @@ def run(A, b, mu, nblock, iter_max, P=1, order=None, err_bound=None, x0=None,
 # ---------------------------------------------------------------------------
 # numpy restatement (small cases only), used to cross-check the C restatement
 # ---------------------------------------------------------------------------
-def run_numpy(A, b, mu, nblock, iter_max, order=None, err_bound=None):
-    A = np.asarray(A, dtype=np.float64)
+def run_numpy(A, b, mu, nblock, iter_max, order=None, err_bound=None, gemv_f32=False):
+    """gemv_f32: A kept in fp32 and the two GEMVs done in fp32 (OpenBLAS sgemv: the reference's
+    TYPE='float' CPU path), everything else in fp64 -- the CPU-baseline variant of SURVEY 8d."""
+    A = np.asarray(A, dtype=np.float32 if gemv_f32 else np.float64)
+    gd = A.dtype
     m, n = A.shape
     w = n // nblock
     b = np.asarray(b, dtype=np.float64).reshape(-1)
-    dg = np.square(A).sum(axis=0).reshape(nblock, w)
+    dg = np.square(A.astype(np.float64) if gemv_f32 else A).sum(axis=0).reshape(nblock, w)
     x = np.zeros((nblock, w))
     Ax = np.zeros((nblock, m))
     err_iter = np.zeros(iter_max)
@@ -132,12 +135,12 @@ def run_numpy(A, b, mu, nblock, iter_max, order=None, err_bound=None):
         mb = int(order[t]) if order is not None else t % nblock
         Am = A[:, mb * w:(mb + 1) * w]
         r = Ax.sum(axis=0) - b
-        g = Am.T @ r
+        g = (Am.T @ r.astype(gd)).astype(np.float64)
         rx = dg[mb] * x[mb] - g
         st = np.sign(rx) * np.maximum(np.abs(rx) - mu, 0)
         Bx = (1.0 / dg[mb]) * st
         D = Bx - x[mb]
-        s23 = Am @ D
+        s23 = (Am @ D.astype(gd)).astype(np.float64)
         r1 = r @ s23 + mu * (np.abs(Bx).sum() - np.abs(x[mb]).sum())
         r2 = s23 @ s23
         gamma = 0.0 if r2 == 0 else float(np.clip(-r1 / r2, 0, 1))
