@@ -666,7 +666,8 @@ def main():
             "workload": workload_label(args, G, m, n_total, ml, w, rows),
             "m": m, "n": n_total, "m_local": ml, "n_local": w, "feature_blocks": args.block,
             "a_storage": args.type, "accumulate": "fp64",
-            "parallelism": f"{'row' if rows else 'column'}-shard x{G}", "split": "rows" if rows else "columns",
+            "parallelism": (f"{'row' if rows else 'column'}-shard x{G}" if G > 1 or args.comm else "single GPU"),
+            "split": ("rows" if rows else "columns") if G > 1 or args.comm else "none",
             "split_rule": "auto: rows for one feature block (one pass over A, DESIGN.md section 6 cost model), "
                           "columns for several" if parse_shard_auto() else "--shard " + args.shard,
             "rccl": bool(G > 1 or args.comm),
