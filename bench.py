@@ -473,6 +473,9 @@ def pmc_traffic(workload_key, kernel):
 MFMA_BF16_DENSE_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 
+LDS_FILL_CAP_GBS = 9600.0   # best LDS-DMA fill rate measured on a panel pass, summed over CUs
+
+
 def panel_bytes_pass(m, w, k):
     """One MFMA pass of the panel path: A_b in bf16 (m x w) once, the k-wide
     operand panel in (hi+lo bf16) and the fp32 split-K output once."""
@@ -534,6 +537,14 @@ def main_panel(args):
     w = pl.MAT_WIDTH
     dom = max(("pass1_mfma", "pass2_mfma"), key=lambda q: kms[q])
     pb = panel_bytes_pass(m, w, k)
+    # bytes through the CU LDS-DMA path per launch: every block streams its A tile and the k-wide
+    # operand over its K range (pass 1: w/256 blocks, each R's ns bf16 pieces over all m rows;
+    # pass 2: m/256 x kchunks blocks, each D' pieces over its w/kchunks columns)
+    ns_dom = 2 if dom == "pass1_mfma" else d_split
+    if dom == "pass1_mfma":
+        fill_bytes = 2 * m * w + (w // 256) * ns_dom * 2 * k * m
+    else:
+        fill_bytes = 2 * m * w + (m // 256) * ns_dom * 2 * k * w
     achieved = pb / (kms[dom] * 1e-3) / 1e9
     # MFMA work of the dominant pass: the residual always enters as hi + lo, the direction
     # as hi + lo (d_split 2) or hi alone (d_split 1)
@@ -582,6 +593,13 @@ def main_panel(args):
             "survey_two_pass_frac": alg_iter / (el_graph / args.steps) / (HBM_PEAK_GBS * 1e9),
             "mfma": {"achieved_tflops": tflops, "peak_tflops": MFMA_BF16_DENSE_TFLOPS,
                      "frac": tflops / MFMA_BF16_DENSE_TFLOPS, "flops_per_launch": flops},
+            # the bound the k-sweep points at: every byte of A and of the k-wide
+            # operand enters LDS through each CU's global_load_lds path; summed over the blocks of a
+            # launch, against the best rate that path sustained in any panel pass (9.6 TB/s = 37.5 GB/s
+            # per CU: pass 2 at k = 128, profiles/r02/final) -- an empirical cap, not a datasheet peak
+            "lds_fill": {"bytes_per_launch": fill_bytes, "achieved_GBps": fill_bytes / (kms[dom] * 1e-3) / 1e9,
+                         "empirical_cap_GBps": LDS_FILL_CAP_GBS,
+                         "frac": fill_bytes / (kms[dom] * 1e-3) / 1e9 / LDS_FILL_CAP_GBS},
         },
     }
     emit(out)
