@@ -117,15 +117,18 @@ def run(A, b, mu, nblock, iter_max, P=1, order=None, err_bound=None, x0=None,
 # ---------------------------------------------------------------------------
 # numpy restatement (small cases only), used to cross-check the C restatement
 # ---------------------------------------------------------------------------
-def run_numpy(A, b, mu, nblock, iter_max, order=None, err_bound=None, gemv_f32=False):
+def run_numpy(A, b, mu, nblock, iter_max, order=None, err_bound=None, gemv_f32=False, dg=None):
     """gemv_f32: A kept in fp32 and the two GEMVs done in fp32 (OpenBLAS sgemv: the reference's
-    TYPE='float' CPU path), everything else in fp64 -- the CPU-baseline variant of SURVEY 8d."""
+    TYPE='float' CPU path), everything else in fp64 -- the CPU-baseline variant of SURVEY 8d.
+    dg: diag(A^T A) computed by the caller (so a timed call holds the iterations only)."""
     A = np.asarray(A, dtype=np.float32 if gemv_f32 else np.float64)
     gd = A.dtype
     m, n = A.shape
     w = n // nblock
     b = np.asarray(b, dtype=np.float64).reshape(-1)
-    dg = np.square(A.astype(np.float64) if gemv_f32 else A).sum(axis=0).reshape(nblock, w)
+    if dg is None:
+        dg = np.square(A.astype(np.float64) if gemv_f32 else A).sum(axis=0)
+    dg = np.asarray(dg, dtype=np.float64).reshape(nblock, w)
     x = np.zeros((nblock, w))
     Ax = np.zeros((nblock, m))
     err_iter = np.zeros(iter_max)
