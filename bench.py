@@ -108,6 +108,8 @@ def parse():
     ap.add_argument("--fused", type=int, default=0, help="1: two-launch fused iteration; 0 (default): five kernels")
     ap.add_argument("--onepass", type=int, default=-1, choices=[-1, 0, 1],
                     help="one pass over A per iteration: -1 (default) when eligible (1 block, 1 rank), 0 off, 1 required")
+    ap.add_argument("--tail-row-blocks", type=int, default=-1, choices=[-1, 0, 1],
+                    help="one-pass tail: residual update on blocks of its own (1, library default) or first in every block (0)")
     ap.add_argument("--onepass-variant", type=int, default=0, help="one-pass ring depth / prefetch variant (0-3)")
     ap.add_argument("--onepass-cache", type=int, default=-1,
                     help="permille of each one-pass row group read with cache-allocating loads (-1: library default)")
@@ -269,6 +271,8 @@ def measure(ctx, args, m, n_total):
     if args.exchange_fp32:
         gc.set_tuning("exchange_fp32", -1)
     gc.set_tuning("onepass_variant", args.onepass_variant)
+    if args.tail_row_blocks >= 0:
+        gc.set_tuning("tail_row_blocks", args.tail_row_blocks)
     if args.onepass_cache >= 0:
         gc.set_tuning("onepass_cache_permille", args.onepass_cache)
 

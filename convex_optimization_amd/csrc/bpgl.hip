@@ -95,6 +95,7 @@ struct bpgl_ctx {
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
     int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
+    int op_rowb = 1;   // k_onepass_tail: residual update on blocks of its own ("tail_row_blocks" knob)
     // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
     // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
     bool rows = false;
@@ -374,8 +375,11 @@ OnePassArgs op_tail_args(const bpgl_ctx* c) {
 }
 template <bool UPDATE>
 int onepass_tail(bpgl_ctx* c) {
-    hipLaunchKernelGGL(k_onepass_tail<UPDATE>, dim3((unsigned)c->op_tail_grid), dim3(kThreads), 0, c->stream,
-                       op_params(c), op_tail_args(c));
+    OnePassArgs o = op_tail_args(c);
+    // the residual update on blocks of its own (about 2 rows per thread, at most kOpTailBlocks blocks)
+    o.rowb = UPDATE && c->op_rowb ? (int)std::min<int64_t>(cdiv(c->m, 2 * kThreads), kOpTailBlocks) : 0;
+    hipLaunchKernelGGL(k_onepass_tail<UPDATE>, dim3((unsigned)(c->op_tail_grid + o.rowb)), dim3(kThreads), 0,
+                       c->stream, op_params(c), o);
     LAUNCH_CHECK("k_onepass_tail");
     return 0;
 }
@@ -1191,6 +1195,12 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->op_variant = (int)value;
         drop_graphs(c);
         c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "tail_row_blocks")) {   // speed only: where the tail's residual update runs (bitwise neutral)
+        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "tail_row_blocks must be 0 or 1");
+        c->op_rowb = (int)value;
+        drop_graphs(c);
         return 0;
     }
     if (!strcmp(key, "onepass_cache_permille")) {

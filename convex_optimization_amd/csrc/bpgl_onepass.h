@@ -65,6 +65,8 @@ struct OnePassArgs {
     const float* Uf;             // row shards, fp32 exchange: the all-reduced U (read instead of Us)
     double* abe;                 // row shards: [sum|Bx|, sum|x|, max err] of the last shrink (k_onepass_fold)
     long long fail_at;           // test hook: iteration whose launch reports a hand-off failure (-1: none)
+    int rowb;                    // k_onepass_tail: blocks appended after the column blocks that only run
+                                 // the residual update (0: the column blocks run it first, as before)
 };
 
 typedef unsigned long long op_u64;
@@ -510,13 +512,21 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
         if (blockIdx.x == 0 && threadIdx.x == 0) finish_step(p, rs, ss, a, b, e);
         if (stop) return;   // block-uniform
     }
-    const long long stride = (long long)gridDim.x * kThreads;
-    const long long k0 = (long long)blockIdx.x * kThreads + threadIdx.x;
+    // the residual update Ax += gamma s23, r = Ax - b (lasso.py:153-155): on `rowb` blocks of its own
+    // (they run beside the column blocks instead of delaying the first of them by a memory round
+    // trip), or, with rowb = 0, by every block before its columns
+    const int cb = (int)gridDim.x - (UPDATE ? o.rowb : 0);   // column blocks
     if (UPDATE) {
-        for (long long k = k0; k < p.m; k += stride) {
-            const double ax = p.Ax[k] + gamma * o.S[k];
-            p.Ax[k] = ax;
-            p.r[k] = ax - p.b[k];
+        const bool own = o.rowb > 0;
+        if (!own || (int)blockIdx.x >= cb) {
+            const long long stride = (long long)(own ? o.rowb : gridDim.x) * kThreads;
+            const long long k0 = (long long)(own ? (int)blockIdx.x - cb : (int)blockIdx.x) * kThreads + threadIdx.x;
+            for (long long k = k0; k < p.m; k += stride) {
+                const double ax = p.Ax[k] + gamma * o.S[k];
+                p.Ax[k] = ax;
+                p.r[k] = ax - p.b[k];
+            }
+            if (own) return;   // block-uniform: row blocks write no shrink partials
         }
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -549,7 +559,7 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
     if (o.ngroups == 1) {
         // row shards (U already summed over ranks): every wave takes its own 64-column tiles
         for (long long tile = (long long)blockIdx.x * kWaves + wave; tile < ntile;
-             tile += (long long)gridDim.x * kWaves) {
+             tile += (long long)cb * kWaves) {
             const long long j = tile * 64 + lane;
             if (j >= p.wp) continue;
             const bool col = j < p.w;
@@ -562,7 +572,7 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
     } else
     // one rank: tiles of 64 (lane = column); the 4 waves split the row-group partials of U
     // (q = wave, wave + 4, ...), wave 0 adds the 4 sums in a fixed order and runs the shrink
-    for (long long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {   // block-uniform
+    for (long long tile = blockIdx.x; tile < ntile; tile += cb) {   // block-uniform
         const long long j = tile * 64 + lane;
         const bool ok = j < p.wp;
         const bool col = ok && j < p.w;

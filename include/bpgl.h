@@ -226,6 +226,8 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   each pass reads last with cache-allocating loads (Infinity Cache reuse by
  *   the other pass).
  *   "reverse_rows" (default 0): the A D pass walks each row chunk bottom-up.
+ *   "tail_row_blocks" (default 1): the one-pass tail runs the residual update on
+ *   blocks of its own, beside its column blocks (0: every block first).
  * These select the iteration's arithmetic path (results agree to rounding,
  * each path is bitwise deterministic):
  *   "onepass" (default -1 = when eligible, 0 = off, 1 = required): one pass

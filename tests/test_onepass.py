@@ -118,6 +118,28 @@ def test_graph_eager_split_steps_bitwise():
     np.testing.assert_array_equal(gc.solver_x(), gc.run(b, mu, 90)["x"])
 
 
+@pytest.mark.parametrize("m", [900, 3001])
+def test_tail_row_blocks_bitwise_neutral(m):
+    """where k_onepass_tail runs the residual update (blocks of its own, the default, or every block
+    first) moves no bit: iterates, err record and the stop point are identical; graph and eager"""
+    rs = np.random.RandomState(m)
+    A = rs.randn(m, 5000)
+    b = rs.randn(m)
+    mu = 0.05 * float(np.abs(A.T @ b).max())
+    gc = make_cls("float")(A, 1, device=0)
+    out = {}
+    for rb in (1, 0):
+        gc.set_tuning("tail_row_blocks", rb)
+        for graph in (True, False):
+            out[rb, graph] = gc.run(b, mu, 120, err_bound=1e-6, record=True, use_graph=graph)
+    for key in out:
+        np.testing.assert_array_equal(out[key]["x"], out[1, True]["x"])
+        np.testing.assert_array_equal(out[key]["err_iter"], out[1, True]["err_iter"])
+        assert out[key]["t_last"] == out[1, True]["t_last"]
+    with pytest.raises(Exception):
+        gc.set_tuning("tail_row_blocks", 2)
+
+
 @pytest.mark.parametrize("refresh", [0, 1, 5, 64])
 def test_refresh_period(refresh):
     """the gradient recurrence with and without exact refreshes: same iterates to rounding"""
