@@ -694,7 +694,6 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     using G = PanelGeo<NT, 2, WNX>;
     __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
