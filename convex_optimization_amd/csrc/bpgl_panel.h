@@ -99,8 +99,6 @@ struct PanelParams {
     long long rec_len;
     PanelState* st;
     unsigned long long* cnt;   // [k] k_panel_reduce arrivals per RHS (monotone: launch q ends at q * groups)
-    float* Gp;          // [2 K-halves][w/512 tiles][...] pass-1 split-K partials of the wide form (k_panel_pass1w)
-    unsigned long long* cnt1;  // [w / 512] k_panel_pass1w arrivals per column tile (monotone: 2 per launch)
     int wt;             // write-through store sites: 1 pass-1 epilogue (x, D'), 2 pass-2 slab, 4 S, 8 R
 };
 
@@ -583,27 +581,24 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 
 // pass-1 epilogue: EPI 0 writes G
 // [k][w] fp64 (API); EPI 1 is the fused shrink -- the direction D' in DS bf16 pieces, the norms
-// per RHS and 256-column tile.  The wave owns output rows c0 + 16 MT wm .. (A columns, MT M-tiles)
-// x RHS tiles wn * NTW ..; 4 waves along the columns; T threads per block; smem holds at least
-// 4 * k * 3 doubles and is free (after a barrier).
-// `acc(mt, nt)` yields the fp32 accumulator tile (M-tile mt, N-tile nt) of this lane.
-template <int NTW, int EPI, int DS, int MT = 4, typename Acc>
+// per RHS and block.  The wave owns output rows c0 + 64 wm .. (A columns) x RHS tiles wn * NTW ..;
+// T threads per block; smem holds at least 4 * k * 3 doubles and is free (after a barrier).
+template <int NTW, int EPI, int DS>
 __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int mb, long long c0, int wm, int wn,
-                                                     int T, Acc&& acc, char* smem, double* __restrict__ Gout) {
-    static_assert(MT == 4 || MT == 8, "64 or 128 columns per wave");
-    constexpr int WPT = 16 / MT;   // waves per 256-column norms tile
+                                                     int T, f32x4 (&acc)[4][NTW], char* smem,
+                                                     double* __restrict__ Gout) {
     const int lane = threadIdx.x & 63;
     const int K = p.k;
     // C layout: row = (lane>>4)*4 + r (A column), col = lane & 15 (RHS)
     if (EPI == 0) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
+        for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
             for (int nt = 0; nt < NTW; ++nt) {
                 const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
-                const long long j = c0 + wm * 16 * MT + mt * 16 + (lane >> 4) * 4;
+                const long long j = c0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) Gout[(long long)rhs * p.w + j + r] = (double)acc(mt, nt)[r];
+                for (int r = 0; r < 4; ++r) Gout[(long long)rhs * p.w + j + r] = (double)acc[mt][nt][r];
             }
         return;
     }
@@ -620,8 +615,8 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         const double gprev = fx ? p.gamma[rhs] : 0.0;
         double sbx = 0.0, sx = 0.0, err = 0.0;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            const long long j = c0 + wm * 16 * MT + mt * 16 + (lane >> 4) * 4;   // 4 consecutive columns
+        for (int mt = 0; mt < 4; ++mt) {
+            const long long j = c0 + wm * 64 + mt * 16 + (lane >> 4) * 4;   // 4 consecutive columns
             float* xp = p.X + ((long long)mb * p.k + rhs) * p.w + j;
             const float4 x4 = *reinterpret_cast<const float4*>(xp);
             float xs[4] = {x4.x, x4.y, x4.z, x4.w};
@@ -639,10 +634,9 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                        make_float4(xs[0], xs[1], xs[2], xs[3]));
             }
             __bf16 dh[4], dl[4];
-            const f32x4 gt = acc(mt, nt);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double g = (double)gt[r];
+                const double g = (double)acc[mt][nt][r];
                 const double x = (double)xs[r];
                 const long long kx = (long long)mb * p.w + j + r;
                 const double bx = p.rec[kx] * soft_thr(p.diag[kx] * x - g, mu);
@@ -676,16 +670,15 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         }
     }
     __syncthreads();
-    for (int u = threadIdx.x; u < K * (4 / WPT); u += T) {   // (256-column tile of this block, RHS)
-        const int rhs = u % K, tl = u / K;
+    for (int rhs = threadIdx.x; rhs < K; rhs += T) {
         double a = 0.0, b = 0.0, e = 0.0;
-        for (int q = tl * WPT; q < (tl + 1) * WPT; ++q) {
+        for (int q = 0; q < 4; ++q) {
             const double* d = nred + ((long long)q * K + rhs) * 3;
             a += d[0];
             b += d[1];
             e = (d[2] > e || d[2] != d[2]) ? d[2] : e;
         }
-        double* dst = p.norms + ((c0 / kPanelRows + tl) * p.k + rhs) * 4;
+        double* dst = p.norms + ((long long)blockIdx.x * p.k + rhs) * 4;
         dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
     }
 }
@@ -715,148 +708,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
         panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                            (int)(p.m / kPanelK), acc);
 
-    panel_pass1_epilogue<G::NTW, EPI, DS>(p, mb, c0, wm, wn, G::T, [&](int mt, int nt) { return acc[mt][nt]; },
-                                          smem, Gout);
-}
-
-// ---------------------------------------------------------------------------
-// pass 1, wide form (interleave1 = 4): a block owns 512 A columns x all k RHS over HALF of the
-// rows (split-K = 2), so each block streams half the residual (the k-wide operand) per A byte of
-// the 256-column form -- the CUs' LDS-DMA fill, which bounds a k = 128 pass, drops
-// from A + R to A + R / 2.  8 waves = 4 (128 columns, 8 M-tiles) x 2 (RHS halves).  A stages are
-// 32 rows deep ([32][1024 B] images, XOR-swizzled like swz512, read with ds_read_b64_tr_b16), the
-// residual stages 64 deep (the 128-B-row image of the other forms), one residual stage per two A
-// stages; three A images and two residual images = 160 KiB at k = 128.  The two K halves of a
-// column tile meet through an fp32 partial slab: the second to arrive (agent-scope release /
-// acquire around a monotone counter, both halves on one XCD) adds the other's partial to its own
-// (P0 + P1 either way: fp32 addition commutes) and runs the usual epilogue.  grid = 2 x w / 512.
-// ---------------------------------------------------------------------------
-// A^T fragment from the [32][1024 B] image: output row = column j0 + (lane & 15), K = 8 (lane >> 4) .. + 7
-__device__ __forceinline__ bf16x8 panel_afrag1w(const char* abuf, int j0, int lane) {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int c = (j0 >> 3) + (p >> 1);
-    const int r0 = 8 * g + q;
-    const int r1 = r0 + 4;
-    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(abuf + r0 * 1024 + 16 * swz512(r0, c) + 8 * (p & 1)));
-    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(abuf + r1 * 1024 + 16 * swz512(r1, c) + 8 * (p & 1)));
-    typedef short s16x8 __attribute__((ext_vector_type(8)));
-    const s16x8 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, v);
-}
-template <int NT, int EPI, int DS>
-__global__ __launch_bounds__(512) void k_panel_pass1w(PanelParams p, int fixed_block, double* __restrict__ Gout) {
-    using G = PanelGeo<NT, 2, 0>;
-    static_assert(G::NW == 8 && G::NTW * 2 == NT, "8 waves, 2 along the RHS");
-    constexpr int MT = 8, NTW = G::NTW;
-    constexpr int AST = 32 * 1024;                     // A stage: 32 rows x 512 columns bf16
-    constexpr int LA = AST / (512 * 16);               // 4 pieces (rows) per wave
-    constexpr int LO = G::OStage / (512 * 16);         // residual pieces per wave (every wave: k >= 32)
-    static_assert(LO * 512 * 16 == G::OStage && LO >= 1, "residual stage must give every wave its pieces");
-    static_assert(3 * AST + 2 * G::OStage <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(16))) char smem[3 * AST + 2 * G::OStage];
-    char* abufs = smem;
-    char* obufs = smem + 3 * AST;
-    const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    const int ntl = (int)(p.w / 512);
-    const int tile = blockIdx.x % ntl, kh = blockIdx.x / ntl;   // ntl % 8 == 0: both halves on one XCD
-    const long long c0 = (long long)tile * 512;
-    const long long kb = (long long)kh * (p.m / 2);
-    const int nsteps = (int)(p.m / 64);                          // 32-row A stages per half
-    const __bf16* acol = p.A + (long long)mb * p.w + c0;
-    f32x4 acc[MT][NTW];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto issue_a = [&](int s) {   // A rows kb + 32 s .. + 31 -> image s % 3 (row = i * 8 + wave)
-        const int sc = s < nsteps ? s : nsteps - 1;              // clamped tail: loads into an unread image
-#pragma unroll
-        for (int i = 0; i < LA; ++i) {
-            const int row = i * 8 + wave;
-            glds16a(acol + (kb + 32ll * sc + row) * p.lda + 8 * swz512(row, lane), abufs + (s % 3) * AST + row * 1024);
-        }
-    };
-    auto issue_o = [&](int u) {   // residual K = kb + 64 u .. + 63 -> image u & 1
-        const int uc = u < nsteps / 2 ? u : nsteps / 2 - 1;
-#pragma unroll
-        for (int i = 0; i < LO; ++i)
-            panel_op_piece<NT, 2, 0>(i, p.Rh, p.Rl, p.ldr, kb + 64ll * uc, obufs + (u & 1) * G::OStage, wave, lane);
-    };
-    // prologue: O(0), A(0), A(1)
-    issue_o(0);
-    issue_a(0);
-    issue_a(1);
-    for (int s = 0; s < nsteps; ++s) {
-        // stage s's data landed: a wave's youngest operations are the pieces issued in stage s - 1
-        // (A(s + 1), and after an even stage also O((s + 1) / 2))
-        if (s & 1) wait_vm_barrier<LA + LO>();
-        else wait_vm_barrier<LA>();
-        issue_a(s + 2);
-        if (!(s & 1)) issue_o(s / 2 + 1);
-        const char* ab = abufs + (s % 3) * AST;
-        const char* ob = obufs + ((s >> 1) & 1) * G::OStage;
-        const int h = s & 1;                                     // K half of the 64-deep residual stage
-        bf16x8 bhi[NTW], blo[NTW];
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-            const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
-            bhi[nt] = panel_bfrag(ob, rhs, h, lane);
-            blo[nt] = panel_bfrag(ob, G::K + rhs, h, lane);
-        }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            const bf16x8 af = panel_afrag1w(ab, wm * 128 + mt * 16, lane);
-#pragma unroll
-            for (int nt = 0; nt < NTW; ++nt) {
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bhi[nt], acc[mt][nt], 0, 0, 0);
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, blo[nt], acc[mt][nt], 0, 0, 0);
-            }
-        }
-    }
-    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free
-    // split-K hand-off: this half's partial, register-index-major ([mt][nt][thread] float4: 1 KiB per
-    // wave-instruction), then the arrival; the second arrival folds the other half in
-    float* mine = p.Gp + ((long long)kh * ntl + tile) * (MT * NTW * 512 * 4);
-    float* other = p.Gp + ((long long)(1 - kh) * ntl + tile) * (MT * NTW * 512 * 4);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)
-            *reinterpret_cast<f32x4*>(mine + ((mt * NTW + nt) * 512 + threadIdx.x) * 4) = acc[mt][nt];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned long long old = __hip_atomic_fetch_add(p.cnt1 + tile, 1ull, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-        const int last = ((old + 1) & 1ull) == 0;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;   // block-uniform: the first half to arrive is done
-    __syncthreads();   // flag read by every thread before the epilogue reuses smem
-    // both halves from the slab, element by element (the accumulators are dead: the epilogue's
-    // registers are free), summed P0 + P1
-    const float* p0 = kh == 0 ? mine : other;
-    const float* p1 = kh == 0 ? other : mine;
-    panel_pass1_epilogue<NTW, EPI, DS, MT>(
-        p, mb, c0, wm, wn, 512,
-        [&](int mt, int nt) {
-            const long long e = ((long long)(mt * NTW + nt) * 512 + threadIdx.x) * 4;
-            return *reinterpret_cast<const f32x4*>(p0 + e) + *reinterpret_cast<const f32x4*>(p1 + e);
-        },
-        smem, Gout);
+    panel_pass1_epilogue<G::NTW, EPI, DS>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
 }
 
 // ---------------------------------------------------------------------------

@@ -46,7 +46,7 @@ struct bpgl_panel {
 namespace {
 
 struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, Gp, cnt1, total;
+    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -71,8 +71,6 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.gamma = k.take(8 * c->k);
     L.err_rhs = k.take(8 * c->k);
     L.cnt = k.take(8 * c->k);
-    L.Gp = k.take(4 * 2 * kw);                          // pass-1 wide form: two K halves of fp32 partials
-    L.cnt1 = k.take(8 * std::max<int64_t>(1, c->w / 512));
     L.total = k.off;
     return L;
 }
@@ -83,14 +81,6 @@ template <int NT, int ILV, int NS, int WNX>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
         case 0:
-            if constexpr (ILV == 4) {   // wide split-K form (eligibility checked by panel_launch_ilv)
-                if (mode) hipLaunchKernelGGL((k_panel_pass1w<NT, 1, NS>), dim3((unsigned)(2 * (c->w / 512))), dim3(512),
-                                             0, c->stream, c->p, fixed_block, out);
-                else hipLaunchKernelGGL((k_panel_pass1w<NT, 0, 2>), dim3((unsigned)(2 * (c->w / 512))), dim3(512), 0,
-                                        c->stream, c->p, fixed_block, out);
-                LAUNCH_CHECK("k_panel_pass1w");
-                break;
-            }
             if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX>), dim3((unsigned)(c->w / kPanelRows)),
                                          dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
             else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX>), dim3((unsigned)(c->w / kPanelRows)),
@@ -111,11 +101,6 @@ int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int
         case 0: return panel_launch_nt<NT, 0, NS, WNX>(c, which, fixed_block, out, mode);
         case 1: return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
         case 2: return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
-        case 4:   // pass 1 only: the wide split-K form (512-column tiles, k >= 32, w a multiple of 4096)
-            if constexpr (NT >= 2 && WNX == 0)
-                if (which == 0 && c->w % 4096 == 0 && c->m % 128 == 0)
-                    return panel_launch_nt<NT, 4, NS, WNX>(c, which, fixed_block, out, mode);
-            return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
         default:
             if constexpr (NT == 8 && WNX == 0) return panel_launch_nt<NT, 3, NS, WNX>(c, which, fixed_block, out, mode);
             else return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
@@ -299,8 +284,6 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.gamma = (double*)(s + L.gamma);
     p.err_rhs = (double*)(s + L.err_rhs);
     p.cnt = (unsigned long long*)(s + L.cnt);
-    p.Gp = (float*)(s + L.Gp);
-    p.cnt1 = (unsigned long long*)(s + L.cnt1);
     p.wt = c->wt;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
@@ -457,7 +440,7 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     if (!c || !key) return fail(BPGL_E_ARG, "null argument");
     const bool both = !strcmp(key, "interleave");
     if (both || !strcmp(key, "interleave1") || !strcmp(key, "interleave2")) {
-        if (value < 0 || value > 4) return fail(BPGL_E_ARG, "interleave must be 0 ... 4");
+        if (value < 0 || value > 3) return fail(BPGL_E_ARG, "interleave must be 0, 1, 2 or 3");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
     } else if (!strcmp(key, "waves") || !strcmp(key, "waves1") || !strcmp(key, "waves2")) {
