@@ -374,10 +374,10 @@ def cpu_baseline(gc, b, mu, seconds, cores, cpu_info, share_note=""):
     t0 = time.perf_counter()
     oracle.run(A, bh, mu, gc.Block, iters, nthreads=threads)
     el = time.perf_counter() - t0
-    out = {"value": iters / el, "unit": "iters/s", "cores": threads, "kind": "port",
-           "sample": f"oracle/bpgl_oracle.c oracle_run, {iters} iterations from x=0 on the same "
-                     f"{H}x{gc.Block * W} fp32 A and b{share_note}, {threads} OpenMP threads (fp64 arithmetic)",
-           "host": cpu_info}
+    c_oracle = {"value": iters / el, "unit": "iters/s", "threads": threads,
+                "sample": f"oracle/bpgl_oracle.c oracle_run, {iters} iterations from x=0 on the same "
+                          f"{H}x{gc.Block * W} fp32 A and b{share_note}, {threads} OpenMP threads (fp64 arithmetic)"}
+    out = {"host": cpu_info, "c_oracle": c_oracle}
     # SURVEY 8d also asks for the numpy restatement (OpenBLAS GEMVs, fp64) beside it: a few
     # iterations, bounded to about a third of the C sample's time
     # iterations only: diag(A^T A) (the set-up, as the reference excludes it: lasso.py:98) is
@@ -397,6 +397,13 @@ def cpu_baseline(gc, b, mu, seconds, cores, cpu_info, share_note=""):
     out["numpy_fp64"] = {"value": v, "unit": "iters/s",
                          "threads": "OpenBLAS default (OMP_NUM_THREADS=" + os.environ.get("OMP_NUM_THREADS", "unset") + ")",
                          "sample": f"oracle.run_numpy, {n_np} iterations from x=0 on the same A (as fp64), set-up excluded"}
+    # the reported baseline: the reference's own CPU arithmetic (cpu_calculation.py's numpy GEMVs at
+    # its default TYPE double, lasso.py:102-157) restated, on this job's cores -- the fastest of the
+    # fp64 CPU paths timed here; the C oracle and the fp32-storage variant stay beside it
+    out.update({"value": v, "unit": "iters/s", "cores": threads, "kind": "port",
+                "sample": f"oracle.run_numpy (the reference iteration in numpy, fp64 OpenBLAS GEMVs), {n_np} "
+                          f"iterations from x=0 on the same {H}x{gc.Block * W} A and b{share_note}, "
+                          f"set-up (diag) excluded, OpenBLAS on {threads} threads"})
     # and the fp32-storage variant (the reference's TYPE='float' CPU path: sgemv on fp32 A, fp64 elsewhere)
     del A64
     v, n_np = numpy_rate(A, seconds / 3, gemv_f32=True)
