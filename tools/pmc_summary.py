@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Average every PMC counter per kernel over the counter_collection CSVs under DIR.
 
-Usage: python tools/pmc_summary.py DIR
+Usage: python tools/pmc_summary.py DIR [DIR ...]
 Prints kernel -> {counter: mean per dispatch}; FETCH_SIZE / WRITE_SIZE are also
 shown as bytes with the gfx950 corrections of MI355X_MICROARCH.md (KiB units;
 FETCH_SIZE x2 for 16-B/lane streaming reads).
@@ -22,9 +22,10 @@ def short(name):
 
 
 def main():
-    root = sys.argv[1]
     vals = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    files = [f for root in sys.argv[1:] for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"),
+                                                           recursive=True)]
+    for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 vals[short(row.get("Kernel_Name", ""))][row["Counter_Name"]].append(float(row["Counter_Value"]))
