@@ -780,20 +780,35 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
     double rs = 0.0, ss = 0.0;
     if (i < p.m) {
         double s[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int c = 0; c < p.kchunks; ++c) {
-            const float4 v = *reinterpret_cast<const float4*>(p.Sslab + ((long long)c * p.k + rhs) * p.m + i);
+        // the residual rows for the line-search partials, loaded up front (in flight with the chunk
+        // loads; p.R is a valid buffer in mode 0 too, where they go unused)
+        const double* rp = p.R + (long long)rhs * p.m + i;
+        const double2 r01 = *reinterpret_cast<const double2*>(rp);
+        const double2 r23 = *reinterpret_cast<const double2*>(rp + 2);
+        const float* src = p.Sslab + (long long)rhs * p.m + i;
+        const long long cstride = (long long)p.k * p.m;
+        auto add = [&](const float4& v) {
             s[0] += (double)v.x;
             s[1] += (double)v.y;
             s[2] += (double)v.z;
             s[3] += (double)v.w;
+        };
+        // chunks in groups of 8 with every load of a group issued before its adds (one memory round
+        // trip per group instead of one per chunk; no per-element condition inside a group, which
+        // would make hipcc wait for each load), the adds in chunk order as before
+        int c = 0;
+        for (; c + 8 <= p.kchunks; c += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(src + (c + q) * cstride);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) add(v[q]);
         }
+        for (; c < p.kchunks; ++c) add(*reinterpret_cast<const float4*>(src + c * cstride));
         const long long e = (long long)rhs * p.m + i;
         wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e, make_double2(s[0], s[1]));
         wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e + 2, make_double2(s[2], s[3]));
         if (mode) {
-            const double* r = p.R + (long long)rhs * p.m + i;
-            const double2 r01 = *reinterpret_cast<const double2*>(r);
-            const double2 r23 = *reinterpret_cast<const double2*>(r + 2);
             rs = fma(r01.x, s[0], rs); rs = fma(r01.y, s[1], rs);
             rs = fma(r23.x, s[2], rs); rs = fma(r23.y, s[3], rs);
             ss = fma(s[0], s[0], ss); ss = fma(s[1], s[1], ss);
