@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
-"""Long-horizon parity at the bench shape (configs[1], 8192 x 65536 fp32): the default one-pass
-solver (carried gradient g += gamma A^T (A D), exact refresh every 256 iterations) and the
-two-pass solver on the GPU against the C oracle on the same fp32 A, after ITERS iterations
-(default 2048 = 8 refreshes).  Prints one JSON line (and a heartbeat while the oracle runs).
+"""Long-horizon parity at a bench shape (configs[1], 8192 x 65536 fp32; or configs[3], 1048576 x
+4096 fp32 = 2^32 elements): the default one-pass solver (carried gradient g += gamma A^T (A D),
+exact refresh every 256 iterations) and the two-pass solver on the GPU against the C oracle on
+the same fp32 A, after ITERS iterations (default 2048 = 8 refreshes).  Prints one JSON line (and
+a heartbeat while the oracle runs).
 
-Usage (GPU box, repo root): python3 tools/longrun_parity.py [ITERS] > gpurun_out/longrun.json
+Usage (GPU box, repo root): python3 tools/longrun_parity.py [ITERS] [CONFIG 1|3] > gpurun_out/longrun.json
 """
 import json
 import os
@@ -18,6 +19,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+    cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    m, n, seed = (8192, 65536, 41) if cfg == 1 else (1048576, 4096, 43)
     import numpy as np
     import torch
     from convex_optimization_amd.parameters import device_instance
@@ -27,7 +30,7 @@ def main():
     def rel(a, b):
         return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(np.asarray(b)))
 
-    gc, b, mu, _ = device_instance(8192, 65536, 0.4, 1, TYPE="float", seed=41, device=0)
+    gc, b, mu, _ = device_instance(m, n, 0.4, 1, TYPE="float", seed=seed, device=0)
     one = gc.run(b, mu, iters, record=True)
     st = {k: gc.solver_stat(k) for k in ("onepass", "refreshes", "fallbacks")}
     gc.set_tuning("onepass", 0)
@@ -45,11 +48,12 @@ def main():
     ref = oracle.run(A, bh, mu, 1, iters, nthreads=min(16, os.cpu_count() or 1))
     stop.set()
 
-    def f(x):
-        r = A.astype(np.float64) @ np.asarray(x) - bh
+    def f(x):   # fp64 objective, A converted 65536 rows at a time
+        x = np.asarray(x, dtype=np.float64)
+        r = np.concatenate([A[i:i + 65536].astype(np.float64) @ x for i in range(0, A.shape[0], 65536)]) - bh
         return 0.5 * float(r @ r) + mu * float(np.abs(x).sum())
     f_ref = f(ref["x"])
-    out = {"workload": "configs[1] 8192x65536 fp32, seed 41", "iters": iters, "onepass_stats": st,
+    out = {"workload": f"configs[{cfg}] {m}x{n} fp32, seed {seed}", "iters": iters, "onepass_stats": st,
            "oracle_s": round(time.time() - t0, 1),
            "onepass_vs_oracle_x_rel_l2": rel(one["x"], ref["x"]), "twopass_vs_oracle_x_rel_l2": rel(two["x"], ref["x"]),
            "onepass_vs_twopass_x_rel_l2": rel(one["x"], two["x"]),
