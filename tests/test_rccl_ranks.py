@@ -1,7 +1,7 @@
-"""Two RCCL ranks exchanging through libbpgl's own communicator (column shards: the reference's
+"""Two and four RCCL ranks exchanging through libbpgl's own communicator (column shards: the reference's
 P-way split, cpu_calculation.py:23-27 / lasso.py:101-126; row shards: one feature block).
 
-Both ranks run on the one GPU of the test box as two processes under torch.distributed.run,
+The ranks run on the one GPU of the test box as separate processes under torch.distributed.run,
 each announcing its own NCCL_HOSTID so RCCL accepts them (the all-reduce then crosses loopback
 sockets instead of xGMI: correctness only, no timing).  Unlike tests/test_rowshard.py, whose
 multi-rank cases sum the exchange buffers in the test, here the product's ncclAllReduce (inside
@@ -48,11 +48,11 @@ def rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
 
 
-@pytest.mark.parametrize("case", ["c1_b2_p4_f32in", "bound_b4_p2_f32in"])
-def test_two_rccl_ranks_column_shards(golden, case, tmp_path):
+@pytest.mark.parametrize("case,world", [("c1_b2_p4_f32in", 2), ("bound_b4_p2_f32in", 2), ("c1_b2_p4_f32in", 4)])
+def test_two_rccl_ranks_column_shards(golden, case, world, tmp_path):
     from convex_optimization_amd import distributed as D
     fx = golden(case)
-    out = _launch(case, "columns", tmp_path)
+    out = _launch(case, "columns", tmp_path, world)
     for tag in ("graph", "eager"):
         x = D.assemble_x([o[f"x_{tag}"] for o in out], int(fx["BLOCK"]))
         assert rel(x, fx["x"]) <= 1e-9, (tag, rel(x, fx["x"]))
@@ -60,17 +60,21 @@ def test_two_rccl_ranks_column_shards(golden, case, tmp_path):
             assert int(o[f"t_last_{tag}"]) == int(fx["t_last"]) and bool(o[f"stopped_{tag}"]) == bool(fx["stopped"])
         T = int(fx["t_last"]) + 1
         np.testing.assert_allclose(out[0][f"err_{tag}"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
-        np.testing.assert_array_equal(out[0][f"err_{tag}"][:T], out[1][f"err_{tag}"][:T])
+        for o in out[1:]:
+            np.testing.assert_array_equal(out[0][f"err_{tag}"][:T], o[f"err_{tag}"][:T])
     np.testing.assert_array_equal(out[0]["x_graph"], out[0]["x_eager"])
 
 
-def test_two_rccl_ranks_row_shards(golden, tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rccl_ranks_row_shards(golden, world, tmp_path):
     fx = golden("c1_b1_p1_f32in")
-    out = _launch("c1_b1_p1_f32in", "rows", tmp_path)
-    np.testing.assert_array_equal(out[0]["diag"], out[1]["diag"])      # all-reduced column norms
+    out = _launch("c1_b1_p1_f32in", "rows", tmp_path, world)
+    for o in out[1:]:
+        np.testing.assert_array_equal(out[0]["diag"], o["diag"])      # all-reduced column norms
     np.testing.assert_allclose(out[0]["diag"], fx["d_ATA"].reshape(-1), rtol=1e-12)
     for tag in ("graph", "eager"):
-        np.testing.assert_array_equal(out[0][f"x_{tag}"], out[1][f"x_{tag}"])   # x replicated bit for bit
+        for o in out[1:]:
+            np.testing.assert_array_equal(out[0][f"x_{tag}"], o[f"x_{tag}"])   # x replicated bit for bit
         assert rel(out[0][f"x_{tag}"], fx["x"]) <= 1e-9, (tag, rel(out[0][f"x_{tag}"], fx["x"]))
         T = int(fx["ITER_MAX"])
         np.testing.assert_allclose(out[0][f"err_{tag}"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
