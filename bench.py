@@ -494,6 +494,16 @@ def panel_bytes_pass(m, w, k):
     return 2 * m * w + 4 * k * (m + w) + 4 * k * (m + w)
 
 
+def panel_fill_bytes(m, w, k, which, d_split=2):
+    """Bytes through the CUs' LDS-DMA path per launch of panel pass `which` (1 or 2): every block
+    streams its A tile and the k-wide operand over its K range -- pass 1: w/256 blocks, each the
+    residual's hi + lo bf16 pieces over all m rows; pass 2: m/256 row blocks x the column chunks,
+    together the direction's d_split pieces over all w columns once per row block."""
+    if which == 1:
+        return 2 * m * w + (w // 256) * 2 * 2 * k * m
+    return 2 * m * w + (m // 256) * d_split * 2 * k * w
+
+
 def main_panel(args):
     """configs[4]: k right-hand sides on m x n bf16 A (PanelLasso, MFMA passes)."""
     import numpy as np
@@ -549,14 +559,7 @@ def main_panel(args):
     w = pl.MAT_WIDTH
     dom = max(("pass1_mfma", "pass2_mfma"), key=lambda q: kms[q])
     pb = panel_bytes_pass(m, w, k)
-    # bytes through the CU LDS-DMA path per launch: every block streams its A tile and the k-wide
-    # operand over its K range (pass 1: w/256 blocks, each R's ns bf16 pieces over all m rows;
-    # pass 2: m/256 x kchunks blocks, each D' pieces over its w/kchunks columns)
-    ns_dom = 2 if dom == "pass1_mfma" else d_split
-    if dom == "pass1_mfma":
-        fill_bytes = 2 * m * w + (w // 256) * ns_dom * 2 * k * m
-    else:
-        fill_bytes = 2 * m * w + (m // 256) * ns_dom * 2 * k * w
+    fill_bytes = panel_fill_bytes(m, w, k, 1 if dom == "pass1_mfma" else 2, d_split)
     achieved = pb / (kms[dom] * 1e-3) / 1e9
     # MFMA work of the dominant pass: the residual always enters as hi + lo, the direction
     # as hi + lo (d_split 2) or hi alone (d_split 1)

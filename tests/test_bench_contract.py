@@ -31,6 +31,16 @@ def test_pass_bytes_and_panel_figures():
     assert b.panel_bytes_pass(8192, 65536, 128) == 2 * 8192 * 65536 + 8 * 128 * (8192 + 65536)
 
 
+def test_panel_fill_bytes():
+    """roofline.lds_fill of the configs[4] line: A plus every block's copy of the k-wide operand"""
+    b = _bench()
+    m, w, k = 8192, 65536, 128
+    assert b.panel_fill_bytes(m, w, k, 1) == 2 * m * w + 256 * 4 * k * m == 2 ** 31
+    assert b.panel_fill_bytes(m, w, k, 2) == 2 * m * w + 32 * 4 * k * w == 2 ** 31
+    assert b.panel_fill_bytes(m, w, k, 2, d_split=1) == 2 * m * w + 32 * 2 * k * w
+    assert b.panel_fill_bytes(m, w, 16, 1) < b.panel_fill_bytes(m, w, 128, 1)
+
+
 def test_onepass_bytes():
     """one pass over A per iteration: the same vector I/O, A read once (roofline ~3720 it/s)"""
     b = _bench()
