@@ -231,35 +231,25 @@ __device__ __forceinline__ bf16x8 panel_afrag1(const char* abuf, int j0, int h, 
 // `a_row0`/`a_col0`: PASS 1 -> (first A row of K, first column of the tile); PASS 2 -> (first row, first column of K).
 // ILV 0: a stage's LDS-DMA pieces are issued together after the barrier; ILV 1: they
 // are spread over the stage's MFMA groups (one scheduling group each).  NS: operand pieces.
-// ILV 4 / 5 (6: the pipelined form below): the forms of ILV 0 / 1 with the two streams' depths swapped -- the k-wide operand
-// (an L2 hit that every block re-reads) triple-buffered and issued two stages ahead, A
-// double-buffered one stage ahead; a stage issues A(s+1) before op(s+2), so the counted wait
-// leaves the youngest LO pieces (op(s+1)) in flight.  Same LDS bytes at k = 128 (2 x 32 + 3 x 32
-// KiB), same arithmetic order (bitwise identical results).
 template <int NT, int PASS, int ILV, int NS, int WNX>
 __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restrict__ A, long long lda,
                                                long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
                                                const __bf16* __restrict__ bl, long long ldb, long long b_k0,
                                                int nsteps, f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
     using G = PanelGeo<NT, NS, WNX>;
-    constexpr bool SW = ILV >= 4;                   // operand two stages ahead, A one
-    constexpr int SPREAD = ILV & 1;
-    static_assert(!SW || G::LO * G::T * 16 == G::OStage, "swapped depths: every wave issues LO operand pieces");
-    static_assert(!SW || 2 * kPanelAStage + 3 * G::OStage <= G::Smem, "swapped depths: LDS budget");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
     char* abufs = smem;
-    char* obufs = smem + (SW ? 2 : kPanelNA) * kPanelAStage;
+    char* obufs = smem + kPanelNA * kPanelAStage;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // piece i of stage (so, sa): i < LO -> k-wide piece, else A piece i - LO (this order is what
-    // the counted wait below assumes: the youngest LA operations are A pieces).  SW: the order is
-    // mirrored (i < LA -> A piece, else k-wide piece i - LA; the youngest LO are k-wide pieces).
-    auto raw_piece = [&](int i, int so, int bo, int sa, int ba) {
+    // the counted wait below assumes: the youngest LA operations are A pieces)
+    auto piece = [&](int i, int so, int bo, int sa, int ba) {
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
@@ -273,46 +263,34 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
                                     abufs + ba * kPanelAStage, wave, lane);
         }
     };
-    auto piece = [&](int i, int so, int bo, int sa, int ba) {
-        raw_piece(SW ? (i < G::LA ? i + G::LO : i - G::LA) : i, so, bo, sa, ba);
-    };
     auto issue_a = [&](int s, int buf) {
 #pragma unroll
-        for (int i = G::LO; i < G::LO + G::LA; ++i) raw_piece(i, 0, 0, s, buf);
+        for (int i = G::LO; i < G::LO + G::LA; ++i) piece(i, 0, 0, s, buf);
     };
     auto issue_o = [&](int s, int buf) {
 #pragma unroll
-        for (int i = 0; i < G::LO; ++i) raw_piece(i, s, buf, 0, 0);
+        for (int i = 0; i < G::LO; ++i) piece(i, s, buf, 0, 0);
     };
     constexpr int NP = G::LO + G::LA;
     constexpr int NG = 2 * G::NTW;                 // MFMA groups per stage
     constexpr int PPG = (NP + NG - 1) / NG;         // pieces per group (ILV)
     // prologue: op(0), A(0), A(1) -- the loop's counted wait assumes exactly this issue order
-    // (SW: A(0), op(0), op(1))
-    if constexpr (SW) {
-        issue_a(0, 0);
-        issue_o(0, 0);
-        issue_o(nsteps > 1 ? 1 : 0, 1);
-    } else {
-        issue_o(0, 0);
-        issue_a(0, 0);
-        issue_a(nsteps > 1 ? 1 : 0, 1);
-    }
-    int abuf = 0, obuf = 0;   // buffers of stage s (SW: A s & 1, op s % 3; else A s % 3, op s & 1)
+    issue_o(0, 0);
+    issue_a(0, 0);
+    issue_a(nsteps > 1 ? 1 : 0, 1);
+    int abuf = 0;
     for (int s = 0; s < nsteps; ++s) {
         // everything but A(s+1) has landed (op(s), A(s)); every wave is past stage s-1's reads
-        // (SW: everything but op(s+1))
-        wait_vm_barrier<SW ? G::LO : G::LA>();
-        const int so = s + (SW ? 2 : 1) < nsteps ? s + (SW ? 2 : 1) : nsteps - 1;   // clamped tail: loads into
-        const int sa = s + (SW ? 1 : 2) < nsteps ? s + (SW ? 1 : 2) : nsteps - 1;   // unread buffers
-        const int bo = SW ? (obuf == 0 ? 2 : obuf - 1) : (s + 1) & 1;   // (s + 2) % 3 or (s + 1) % 2
-        const int ba = SW ? (s + 1) & 1 : (abuf == 0 ? 2 : abuf - 1);
-        if (!SPREAD) {
+        wait_vm_barrier<G::LA>();
+        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
+        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
+        if (!ILV) {
 #pragma unroll
             for (int i = 0; i < NP; ++i) piece(i, so, bo, sa, ba);
         }
         const char* ab = abufs + abuf * kPanelAStage;
-        const char* ob = obufs + obuf * G::OStage;
+        const char* ob = obufs + (s & 1) * G::OStage;
         static_for<0, 2>([&](auto hc) {
             constexpr int h = decltype(hc)::value;
             bf16x8 af[4];
@@ -325,7 +303,7 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
                 constexpr int grp = h * G::NTW + nt;
                 constexpr int p0 = grp * PPG < NP ? grp * PPG : NP;
                 constexpr int p1 = (grp + 1) * PPG < NP ? (grp + 1) * PPG : NP;
-                if constexpr (SPREAD) {
+                if constexpr (ILV) {
                     static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
                 }
                 const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
@@ -338,19 +316,13 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
                     if constexpr (NS == 2)
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
                 }
-                if constexpr (SPREAD) {
+                if constexpr (ILV) {
                     if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
                     __builtin_amdgcn_sched_group_barrier(0x8, 4 * NS, 0);
                 }
             });
         });
-        if constexpr (SW) {
-            abuf ^= 1;
-            obuf = obuf == 2 ? 0 : obuf + 1;
-        } else {
-            abuf = abuf == 2 ? 0 : abuf + 1;
-            obuf ^= 1;
-        }
+        abuf = abuf == 2 ? 0 : abuf + 1;
     }
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
@@ -361,25 +333,23 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 // reuse is unchanged (a stage's buffers are refilled only after the barrier that follows
 // all of its reads); all LDS-DMA pieces of a stage are issued before its barrier, spread
 // over the first G - 1 groups.
-template <int NT, int PASS, int NS, int WNX, bool SW = false>
+template <int NT, int PASS, int NS, int WNX>
 __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __restrict__ A, long long lda,
                                                     long long a_row0, long long a_col0,
                                                     const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
                                                     long long ldb, long long b_k0, int nsteps,
                                                     f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
     using G = PanelGeo<NT, NS, WNX>;
-    static_assert(!SW || G::LO * G::T * 16 == G::OStage, "swapped depths: every wave issues LO operand pieces");
-    static_assert(!SW || 2 * kPanelAStage + 3 * G::OStage <= G::Smem, "swapped depths: LDS budget");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
     char* abufs = smem;
-    char* obufs = smem + (SW ? 2 : kPanelNA) * kPanelAStage;
+    char* obufs = smem + kPanelNA * kPanelAStage;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto raw_piece = [&](int i, int so, int bo, int sa, int ba) {
+    auto piece = [&](int i, int so, int bo, int sa, int ba) {
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
@@ -392,9 +362,6 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
             panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
                                     abufs + ba * kPanelAStage, wave, lane);
         }
-    };
-    auto piece = [&](int i, int so, int bo, int sa, int ba) {   // SW: A pieces first, operand last
-        raw_piece(SW ? (i < G::LA ? i + G::LO : i - G::LA) : i, so, bo, sa, ba);
     };
     constexpr int NP = G::LO + G::LA;
     constexpr int NG = 2 * G::NTW;                                  // MFMA groups per stage (h, nt)
@@ -412,33 +379,23 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
         if constexpr (NS == 2) blo = panel_bfrag(ob, G::K + rhs, h, lane);
     };
 
-    // prologue: op(0), A(0), A(1) (SW: A(0), op(0), op(1)), then stage 0 landed and group 0's
-    // fragments read
-    if constexpr (SW) {
-        for (int i = G::LO; i < NP; ++i) raw_piece(i, 0, 0, 0, 0);
-        for (int i = 0; i < G::LO; ++i) raw_piece(i, 0, 0, 0, 0);
-        for (int i = 0; i < G::LO; ++i) raw_piece(i, nsteps > 1 ? 1 : 0, 1, 0, 0);
-    } else {
-        for (int i = 0; i < G::LO; ++i) raw_piece(i, 0, 0, 0, 0);
-        for (int i = G::LO; i < NP; ++i) raw_piece(i, 0, 0, 0, 0);
-        for (int i = G::LO; i < NP; ++i) raw_piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
-    }
-    wait_vm_barrier<SW ? G::LO : G::LA>();
+    // prologue: op(0), A(0), A(1), then stage 0 landed and group 0's fragments read
+    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
+    wait_vm_barrier<G::LA>();
     bf16x8 af[2][4];
     bf16x8 bfr[2][2];
     read_a(abufs, 0, af[0]);
     read_b(obufs, 0, 0, bfr[0][0], bfr[0][1]);
-    int abuf = 0, obuf = 0;
+    int abuf = 0;
     for (int s = 0; s < nsteps; ++s) {
-        constexpr int DO = SW ? 2 : 1, DA = SW ? 1 : 2;          // stages ahead: operand, A
-        const int so = s + DO < nsteps ? s + DO : nsteps - 1;    // clamped tail: loads into unread buffers
-        const int sa = s + DA < nsteps ? s + DA : nsteps - 1;
-        const int bo = SW ? (obuf == 0 ? 2 : obuf - 1) : (s + 1) & 1;   // (s + DO) mod buffers
-        const int ba = SW ? (s + 1) & 1 : (abuf == 0 ? 2 : abuf - 1);
-        const int abuf_next = SW ? abuf ^ 1 : (abuf == 2 ? 0 : abuf + 1);
-        const int obuf_next = SW ? (obuf == 2 ? 0 : obuf + 1) : obuf ^ 1;
+        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
+        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
+        const int abuf_next = abuf == 2 ? 0 : abuf + 1;
         const char* ab = abufs + abuf * kPanelAStage;
-        const char* ob = obufs + obuf * G::OStage;
+        const char* ob = obufs + (s & 1) * G::OStage;
         static_for<0, NG>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
             constexpr int h = g / G::NTW, nt = g % G::NTW;
@@ -451,10 +408,10 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
                 if constexpr (h1 != h) read_a(ab, h1, af[h1 & 1]);
                 read_b(ob, h1, nt1, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
             } else {
-                // stage s + 1 landed (only A(s+2), SW: op(s+2), may be outstanding); stage s's reads retired
-                wait_vm_barrier<SW ? G::LO : G::LA>();
+                // stage s + 1 landed (only A(s+2) may be outstanding); stage s's reads retired
+                wait_vm_barrier<G::LA>();
                 const char* abn = abufs + abuf_next * kPanelAStage;
-                const char* obn = obufs + obuf_next * G::OStage;
+                const char* obn = obufs + ((s + 1) & 1) * G::OStage;
                 read_a(abn, 0, af[0]);   // the last group runs on af[1] (h = 1)
                 read_b(obn, 0, 0, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
             }
@@ -466,114 +423,6 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
             }
         });
         abuf = abuf_next;
-        obuf = obuf_next;
-    }
-    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
-}
-
-// Pass 1 with 32-deep stages and a deeper A ring (interleave1 7: NA = 6, 8: NA = 7; k = 128, 8 waves).
-// A stage = 32 rows x 256 columns (16 KiB, full 512-B row segments), operand stage = 2k rows x 64 B
-// (16 KiB); NA A slots and 10 - NA operand slots fill the 160 KiB, so A runs NA - 1 stages (80 or
-// 96 KiB) ahead instead of 64 KiB, and the operand 9 - NA stages (48 / 32 KiB).  A stage issues
-// op(s + DO) then A(s + DA); with DA > DO the counted wait at the top of stage s leaves in flight the
-// full issue of stages s-1 .. s-DO+1 and the A pieces of stage s-DO, so A(s) and op(s) have landed.
-// Same MFMA order per accumulator as the 64-deep forms (K ascending): bitwise identical results.
-// Operand image: 64-B rows, chunk c of row r at slot c ^ (-(r >> 2) & 3) -- conflict-free for the
-// ds_read_b128 lane groups of a 16 x 16 x 32 B fragment.
-__device__ __forceinline__ int swz64(int r, int c) { return c ^ (-(r >> 2) & 3); }
-
-template <int NT, int NA>
-__device__ __forceinline__ void panel_mainloop_k32(char* smem, const __bf16* __restrict__ A, long long lda,
-                                                   long long a_col0, const __bf16* __restrict__ bh,
-                                                   const __bf16* __restrict__ bl, long long ldb, int nsteps,
-                                                   f32x4 (&acc)[4][PanelGeo<NT, 2, 0>::NTW]) {
-    using G = PanelGeo<NT, 2, 0>;
-    constexpr int KS = 32;
-    constexpr int AST = kPanelRows * KS * 2;            // 16 KiB
-    constexpr int OST = 2 * G::K * KS * 2;              // 16 KiB at k = 128
-    constexpr int NO = (G::Smem - NA * AST) / OST;
-    constexpr int DA = NA - 1, DO = NO - 1;
-    constexpr int LA = AST / (G::T * 16), LO = OST / (G::T * 16);
-    static_assert(LA * G::T * 16 == AST && LO * G::T * 16 == OST, "every wave issues whole pieces");
-    static_assert(DA > DO && DO >= 1, "ring depths");
-    static_assert(NA * AST + NO * OST <= G::Smem, "LDS budget");
-    constexpr int WAITN = (DO - 1) * (LO + LA) + LA;
-    static_assert(WAITN <= 63, "vmcnt");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    char* abufs = smem;
-    char* obufs = smem + NA * AST;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // A piece: 2 rows of 512 B (the 64-deep form's piece); operand piece: 16 image rows of 64 B
-    auto a_piece = [&](int q, int st, int slot) {
-        const int pc = q * G::NW + wave;
-        const int row = pc * 2 + (lane >> 5);
-        const int c = swz512(row, lane & 31);
-        glds16a(A + ((long long)st * KS + row) * lda + a_col0 + 8 * c, abufs + slot * AST + pc * 1024);
-    };
-    auto o_piece = [&](int q, int st, int slot) {
-        const int pc = q * G::NW + wave;
-        const int rr = pc * 16 + (lane >> 2);
-        const int c = swz64(rr, lane & 3);
-        const int hl = rr / G::K, rhs = rr % G::K;
-        glds16o((hl ? bl : bh) + (long long)rhs * ldb + (long long)st * KS + 8 * c, obufs + slot * OST + pc * 1024);
-    };
-    auto issue_stage = [&](int so, int bo, int sa, int ba, bool with_op) {   // op first, then A
-        if (with_op) {
-#pragma unroll
-            for (int q = 0; q < LO; ++q) o_piece(q, so, bo);
-        }
-#pragma unroll
-        for (int q = 0; q < LA; ++q) a_piece(q, sa, ba);
-    };
-    // prologue = the issue of virtual stages -DA .. -1 (op only from stage -DO on)
-    for (int v = -DA; v < 0; ++v) {
-        const int sa = v + DA < nsteps ? v + DA : nsteps - 1;
-        const int so = v + DO < nsteps ? v + DO : nsteps - 1;
-        issue_stage(so, (v + DO) % NO, sa, (v + DA) % NA, v + DO >= 0);
-    }
-    constexpr int NG = G::NTW;                          // MFMA groups per stage (one K-half of 32)
-    constexpr int NP = LO + LA;
-    constexpr int PPG = (NP + NG - 1) / NG;
-    int aslot = 0, oslot = 0;
-    for (int s = 0; s < nsteps; ++s) {
-        wait_vm_barrier<WAITN>();                       // A(s), op(s) landed; stage s-1's reads retired
-        const int sa = s + DA < nsteps ? s + DA : nsteps - 1;   // clamped tail: loads into unread slots
-        const int so = s + DO < nsteps ? s + DO : nsteps - 1;
-        const int ba = aslot == 0 ? NA - 1 : aslot - 1;          // (s + DA) % NA
-        const int bo = oslot == 0 ? NO - 1 : oslot - 1;          // (s + DO) % NO
-        const char* ab = abufs + aslot * AST;
-        const char* ob = obufs + oslot * OST;
-        bf16x8 af[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) af[mt] = panel_afrag1(ab, wm * 64 + mt * 16, 0, lane);
-        static_for<0, NG>([&](auto ntc) {
-            constexpr int nt = decltype(ntc)::value;
-            constexpr int p0 = nt * PPG < NP ? nt * PPG : NP;
-            constexpr int p1 = (nt + 1) * PPG < NP ? (nt + 1) * PPG : NP;
-            static_for<p0, p1>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                if constexpr (i < LO) o_piece(i, so, bo);
-                else a_piece(i - LO, sa, ba);
-            });
-            const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
-            const bf16x8 b_hi = *reinterpret_cast<const bf16x8*>(ob + rhs * 64 + 16 * swz64(rhs, lane >> 4));
-            const bf16x8 b_lo =
-                *reinterpret_cast<const bf16x8*>(ob + (G::K + rhs) * 64 + 16 * swz64(G::K + rhs, lane >> 4));
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
-            }
-            if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
-            __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
-        });
-        aslot = aslot == NA - 1 ? 0 : aslot + 1;
-        oslot = oslot == NO - 1 ? 0 : oslot + 1;
     }
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
@@ -849,14 +698,11 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr ((ILV == 7 || ILV == 8) && WNX == 0 && NT == 8)
-        panel_mainloop_k32<NT, ILV == 7 ? 6 : 7>(smem, p.A, p.lda, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr,
-                                                 (int)(p.m / 32), acc);
-    else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+    if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                       (int)(p.m / kPanelK), acc);
-    else if constexpr (ILV == 2 || ILV == 3 || ILV == 6)
-        panel_mainloop_pipe<NT, 1, 2, WNX, ILV == 6>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
+    else if constexpr (ILV >= 2)
+        panel_mainloop_pipe<NT, 1, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                            (int)(p.m / kPanelK), acc);
     else
         panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
@@ -896,8 +742,8 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
     if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);
-    else if constexpr (ILV == 2 || ILV == 3 || ILV == 6)
-        panel_mainloop_pipe<NT, 2, NS, WNX, ILV == 6>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
+    else if constexpr (ILV >= 2)
+        panel_mainloop_pipe<NT, 2, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
                                             p.ldd, chunk * kc, (int)(kc / kPanelK), acc);
     else
         panel_mainloop<NT, 2, ILV, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,

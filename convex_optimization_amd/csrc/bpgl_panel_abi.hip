@@ -101,29 +101,6 @@ int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int
         case 0: return panel_launch_nt<NT, 0, NS, WNX>(c, which, fixed_block, out, mode);
         case 1: return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
         case 2: return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
-        case 4:
-        case 5:
-        case 6: {
-            // swapped stream depths: every wave must issue whole operand pieces (else the form of 1)
-            using G1 = PanelGeo<NT, 2, WNX>;
-            using G2 = PanelGeo<NT, NS, WNX>;
-            if constexpr (G1::LO * G1::T * 16 == G1::OStage && G2::LO * G2::T * 16 == G2::OStage) {
-                if (c->interleave[which] == 4) return panel_launch_nt<NT, 4, NS, WNX>(c, which, fixed_block, out, mode);
-                if (c->interleave[which] == 6) return panel_launch_nt<NT, 6, NS, WNX>(c, which, fixed_block, out, mode);
-                return panel_launch_nt<NT, 5, NS, WNX>(c, which, fixed_block, out, mode);
-            } else {
-                return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
-            }
-        }
-        case 7:
-        case 8:   // pass 1 with 32-deep stages and a deeper A ring (k = 128, 8 waves; else the form of 2)
-            if constexpr (NT == 8 && WNX == 0) {
-                if (which == 0) {
-                    if (c->interleave[0] == 7) return panel_launch_nt<NT, 7, NS, WNX>(c, which, fixed_block, out, mode);
-                    return panel_launch_nt<NT, 8, NS, WNX>(c, which, fixed_block, out, mode);
-                }
-            }
-            return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
         default:
             if constexpr (NT == 8 && WNX == 0) return panel_launch_nt<NT, 3, NS, WNX>(c, which, fixed_block, out, mode);
             else return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
@@ -463,7 +440,7 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     if (!c || !key) return fail(BPGL_E_ARG, "null argument");
     const bool both = !strcmp(key, "interleave");
     if (both || !strcmp(key, "interleave1") || !strcmp(key, "interleave2")) {
-        if (value < 0 || value > 8) return fail(BPGL_E_ARG, "interleave must be 0-8");
+        if (value < 0 || value > 3) return fail(BPGL_E_ARG, "interleave must be 0, 1, 2 or 3");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
     } else if (!strcmp(key, "waves") || !strcmp(key, "waves1") || !strcmp(key, "waves2")) {
