@@ -759,126 +759,6 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
         }
 }
 
-// Pass 2 with the roles split (interleave2 4; k = 128): waves 0-3 only read fragments and issue
-// MFMAs (wave q: rows 64q..64q+63 x all 128 RHS, 32 accumulator tiles), waves 4-7 only issue the
-// LDS-DMA pieces (8 A + 8 operand pieces each per stage) and wait for them to land.  Same buffers,
-// depths and single barrier per stage as panel_mainloop: at the top of stage s the loaders have
-// waited for op(s), A(s) (vmcnt: only their A(s+1) pieces outstanding) and the consumers have
-// retired their stage s-1 reads (lgkmcnt(0)); after it the loaders refill the slots of stage s-1.
-// Per accumulator the MFMA order is the same (K ascending, hi then lo): bitwise identical S.
-template <int NS>
-__global__ __launch_bounds__(512) void k_panel_pass2_rs(PanelParams p, int fixed_block) {
-    constexpr int K = 128, NTW = 8;
-    constexpr int OStage = NS * K * kPanelK * 2;
-    constexpr int LA = kPanelAStage / (4 * 1024), LO = OStage / (4 * 1024);   // pieces per loader and stage
-    static_assert(LA * 4 * 1024 == kPanelAStage && LO * 4 * 1024 == OStage, "whole pieces");
-    static_assert(kPanelNA * kPanelAStage + kPanelNO * OStage <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(16))) char smem[kPanelNA * kPanelAStage + kPanelNO * OStage];
-    const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nrb = (int)(p.m / kPanelRows);
-    int rb = blockIdx.x % nrb, chunk = blockIdx.x / nrb;   // XCD-aware map as k_panel_pass2
-    if (p.kchunks % 8 == 0) {
-        const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-        chunk = xcd * (p.kchunks / 8) + slot / nrb;
-        rb = slot % nrb;
-    } else if (8 % p.kchunks == 0 && nrb % (8 / p.kchunks) == 0) {
-        const int xpc = 8 / p.kchunks, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-        chunk = xcd / xpc;
-        rb = (xcd % xpc) * (nrb / xpc) + slot;
-    }
-    const long long kc = p.w / p.kchunks;
-    const long long r0 = (long long)rb * kPanelRows;
-    const long long acol = (long long)mb * p.w + chunk * kc;   // first A column of the chunk
-    const long long bk0 = chunk * kc;
-    const int nsteps = (int)(kc / kPanelK);
-    char* abufs = smem;
-    char* obufs = smem + kPanelNA * kPanelAStage;
-    if (wave >= 4) {
-        // loader: piece pc = 4 q + lw of a stage (A: 8 rows of 128 B; operand: 8 image rows)
-        const int lw = wave - 4;
-        auto a_piece = [&](int q, int st, int buf) {
-            const int pc = q * 4 + lw;
-            const int row = pc * 8 + (lane >> 3);
-            const int c = swz128(row, lane & 7);
-            glds16a(p.A + (r0 + row) * p.lda + acol + (long long)st * kPanelK + 8 * c,
-                    abufs + buf * kPanelAStage + pc * 1024);
-        };
-        auto o_piece = [&](int q, int st, int buf) {
-            const int pc = q * 4 + lw;
-            const int rr = pc * 8 + (lane >> 3);
-            const int c = swz128(rr, lane & 7);
-            const int hl = rr / K, rhs = rr % K;
-            glds16o((hl ? p.Dl : p.Dh) + (long long)rhs * p.ldd + bk0 + (long long)st * kPanelK + 8 * c,
-                    obufs + buf * OStage + pc * 1024);
-        };
-#pragma unroll
-        for (int q = 0; q < LO; ++q) o_piece(q, 0, 0);
-#pragma unroll
-        for (int q = 0; q < LA; ++q) a_piece(q, 0, 0);
-#pragma unroll
-        for (int q = 0; q < LA; ++q) a_piece(q, nsteps > 1 ? 1 : 0, 1);
-        int abuf = 0;
-        for (int s = 0; s < nsteps; ++s) {
-            wait_vm_barrier<LA>();   // op(s), A(s) landed (only A(s+1) outstanding)
-            const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;   // clamped tail: loads into unread buffers
-            const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
-            const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;
-#pragma unroll
-            for (int q = 0; q < LO; ++q) o_piece(q, so, bo);
-#pragma unroll
-            for (int q = 0; q < LA; ++q) a_piece(q, sa, ba);
-            abuf = abuf == 2 ? 0 : abuf + 1;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads have landed
-        return;
-    }
-    // consumer
-    const int wm = wave;
-    f32x4 acc[4][NTW];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int abuf = 0;
-    for (int s = 0; s < nsteps; ++s) {
-        wait_vm_barrier<0>();    // this wave issues no vector-memory ops: retires its LDS reads, then barrier
-        const char* ab = abufs + abuf * kPanelAStage;
-        const char* ob = obufs + (s & 1) * OStage;
-        static_for<0, 2>([&](auto hc) {
-            constexpr int h = decltype(hc)::value;
-            bf16x8 af[4];
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) af[mt] = panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
-            static_for<0, NTW>([&](auto ntc) {
-                constexpr int nt = decltype(ntc)::value;
-                const int rhs = nt * 16 + (lane & 15);
-                const bf16x8 b_hi = panel_bfrag(ob, rhs, h, lane);
-                bf16x8 b_lo;
-                if constexpr (NS == 2) b_lo = panel_bfrag(ob, K + rhs, h, lane);
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    if constexpr (NS == 2)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
-                }
-            });
-        });
-        abuf = abuf == 2 ? 0 : abuf + 1;
-    }
-    // (the loaders' last barrier is the one at the top of their last stage; consumers need none after)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-            const int rhs = nt * 16 + (lane & 15);
-            const long long row = r0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
-            wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
-                   make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
-        }
-}
-
 __device__ __forceinline__ void panel_st_sc1(double* q, double v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(q), (unsigned long long)__double_as_longlong(v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -112,9 +112,7 @@ def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
     pl = PanelLasso(Ab, 2, nrhs=k, device=0)
     pl.set_tuning("d_split", d_split)
     out = []
-    # 3: the staggered four-phase form (k = 128; others fall back to 2); 4: pass 2 with loader and
-    # MFMA waves split (k = 128; pass 1 and other k: the form of 1)
-    for v in (0, 1, 2, 3, 4):
+    for v in (0, 1, 2, 3):            # 3: the staggered four-phase form (k = 128; others fall back to 2)
         pl.set_tuning("interleave", v)
         out.append(pl.run(B, mu, 12)["x"])
     for o in out[1:]:
