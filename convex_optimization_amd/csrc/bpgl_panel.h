@@ -759,120 +759,6 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
         }
 }
 
-// Pass 2 on 512-row tiles (interleave2 4; k = 128): each of the 8 waves owns 64 rows x all 128 RHS
-// (32 accumulator tiles), so a block streams half the direction bytes per A byte of the 256-row
-// form -- the CU's LDS-DMA fill path, not HBM, bounds a k = 128 pass.  LDS: A double-
-// buffered (2 x 64 KiB, one 512 x 64 stage ahead) and the direction stage as two RHS halves O0
-// (RHS 0-63) and O1 (RHS 64-127) of 16 KiB, each refilled half a stage ahead:
-//   B1(s): A(s), O0(s) landed -> issue O1(s), A(s+1); MFMAs of RHS 0-63 (A(s), O0)
-//   B2(s): O1(s) landed, O0 reads retired -> issue O0(s+1); MFMAs of RHS 64-127 (A(s), O1)
-// Lead times equal the 256-row form's (a stage is twice as long).  Per accumulator the MFMA order is
-// unchanged (K ascending, hi then lo), so with the same kchunks the slab is bitwise that of the
-// 256-row form; the grid is (m / 512) x kchunks (kchunks 16 at configs[4] for one block per CU).
-template <int NS>
-__global__ __launch_bounds__(512) void k_panel_pass2_w(PanelParams p, int fixed_block) {
-    constexpr int NTW = 8, ROWS = 512;
-    constexpr int AST = ROWS * kPanelK * 2;                 // 64 KiB
-    constexpr int OH = NS * 64 * kPanelK * 2;               // one RHS half of a direction stage
-    constexpr int LA = AST / (512 * 16), LOH = OH / (512 * 16);
-    static_assert(LA * 512 * 16 == AST && LOH * 512 * 16 == OH, "whole pieces");
-    static_assert(2 * AST + 2 * OH <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(16))) char smem[2 * AST + 2 * OH];
-    const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nrb = (int)(p.m / ROWS);
-    int rb = blockIdx.x % nrb, chunk = blockIdx.x / nrb;   // XCD-aware map as k_panel_pass2
-    if (p.kchunks % 8 == 0) {
-        const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-        chunk = xcd * (p.kchunks / 8) + slot / nrb;
-        rb = slot % nrb;
-    } else if (8 % p.kchunks == 0 && nrb % (8 / p.kchunks) == 0) {
-        const int xpc = 8 / p.kchunks, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-        chunk = xcd / xpc;
-        rb = (xcd % xpc) * (nrb / xpc) + slot;
-    }
-    const long long kc = p.w / p.kchunks;
-    const long long r0 = (long long)rb * ROWS;
-    const long long acol = (long long)mb * p.w + chunk * kc;
-    const long long bk0 = chunk * kc;
-    const int nsteps = (int)(kc / kPanelK);
-    char* abufs = smem;
-    char* obufs = smem + 2 * AST;
-    auto a_piece = [&](int q, int st, int buf) {   // 8 rows of 128 B
-        const int pc = q * 8 + wave;
-        const int row = pc * 8 + (lane >> 3);
-        const int c = swz128(row, lane & 7);
-        glds16a(p.A + (r0 + row) * p.lda + acol + (long long)st * kPanelK + 8 * c, abufs + buf * AST + pc * 1024);
-    };
-    auto o_piece = [&](int q, int st, int half) {   // 8 image rows ([hl][64 RHS] x 128 B)
-        const int pc = q * 8 + wave;
-        const int rr = pc * 8 + (lane >> 3);
-        const int c = swz128(rr, lane & 7);
-        const int hl = rr >> 6, rhs = half * 64 + (rr & 63);
-        glds16o((hl ? p.Dl : p.Dh) + (long long)rhs * p.ldd + bk0 + (long long)st * kPanelK + 8 * c,
-                obufs + half * OH + pc * 1024);
-    };
-    f32x4 acc[4][NTW];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mfma_half = [&](const char* ab, auto halfc) {
-        constexpr int half = decltype(halfc)::value;
-        const char* ob = obufs + half * OH;
-        static_for<0, 2>([&](auto hc) {
-            constexpr int h = decltype(hc)::value;
-            bf16x8 af[4];
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) af[mt] = panel_afrag2(ab, wave * 64 + mt * 16 + (lane & 15), h, lane);
-            static_for<0, 4>([&](auto ntc) {
-                constexpr int n4 = decltype(ntc)::value;
-                constexpr int nt = half * 4 + n4;
-                const int rr = n4 * 16 + (lane & 15);
-                const bf16x8 b_hi = panel_bfrag(ob, rr, h, lane);
-                bf16x8 b_lo;
-                if constexpr (NS == 2) b_lo = panel_bfrag(ob, 64 + rr, h, lane);
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    if constexpr (NS == 2)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
-                }
-            });
-        });
-    };
-    // prologue: O0(0), A(0)
-#pragma unroll
-    for (int q = 0; q < LOH; ++q) o_piece(q, 0, 0);
-#pragma unroll
-    for (int q = 0; q < LA; ++q) a_piece(q, 0, 0);
-    for (int s = 0; s < nsteps; ++s) {
-        wait_vm_barrier<0>();                                   // B1(s)
-        const int s1 = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
-#pragma unroll
-        for (int q = 0; q < LOH; ++q) o_piece(q, s, 1);
-#pragma unroll
-        for (int q = 0; q < LA; ++q) a_piece(q, s1, (s + 1) & 1);
-        const char* ab = abufs + (s & 1) * AST;
-        mfma_half(ab, std::integral_constant<int, 0>{});
-        wait_vm_barrier<LA>();                                  // B2(s): O1(s) landed (A(s+1) may be in flight)
-#pragma unroll
-        for (int q = 0; q < LOH; ++q) o_piece(q, s1, 0);
-        mfma_half(ab, std::integral_constant<int, 1>{});
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // the clamped tail loads have landed
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-            const int rhs = nt * 16 + (lane & 15);
-            const long long row = r0 + wave * 64 + mt * 16 + (lane >> 4) * 4;
-            wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
-                   make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
-        }
-}
-
 __device__ __forceinline__ void panel_st_sc1(double* q, double v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(q), (unsigned long long)__double_as_longlong(v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -101,16 +101,6 @@ int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int
         case 0: return panel_launch_nt<NT, 0, NS, WNX>(c, which, fixed_block, out, mode);
         case 1: return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
         case 2: return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
-        case 4:   // pass 2 on 512-row tiles (k = 128, 8 waves, m % 512 == 0; else the form of 1)
-            if constexpr (NT == 8 && WNX == 0) {
-                if (which == 1 && c->m % 512 == 0) {
-                    hipLaunchKernelGGL((k_panel_pass2_w<NS>), dim3((unsigned)((c->m / 512) * c->kchunks)), dim3(512),
-                                       0, c->stream, c->p, fixed_block);
-                    LAUNCH_CHECK("k_panel_pass2_w");
-                    return 0;
-                }
-            }
-            return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
         default:
             if constexpr (NT == 8 && WNX == 0) return panel_launch_nt<NT, 3, NS, WNX>(c, which, fixed_block, out, mode);
             else return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
@@ -450,7 +440,7 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     if (!c || !key) return fail(BPGL_E_ARG, "null argument");
     const bool both = !strcmp(key, "interleave");
     if (both || !strcmp(key, "interleave1") || !strcmp(key, "interleave2")) {
-        if (value < 0 || value > 4) return fail(BPGL_E_ARG, "interleave must be 0-4");
+        if (value < 0 || value > 3) return fail(BPGL_E_ARG, "interleave must be 0, 1, 2 or 3");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
     } else if (!strcmp(key, "waves") || !strcmp(key, "waves1") || !strcmp(key, "waves2")) {

@@ -187,7 +187,7 @@ class PanelLasso:
         return self.solver_x_device().to(torch.float64).cpu().numpy().T.copy()   # (n, k)
 
     def set_tuning(self, key, value):
-        """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave' 0-4.
+        """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave' 0-2.
         'd_split' 1 / 2: the solver's direction enters the A D pass as its bf16 rounding (1) or as a
         hi + lo pair (2); both are exact line searches along the direction taken."""
         N.check(_lib().bpgl_panel_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_panel_set_tuning")

@@ -112,9 +112,7 @@ def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
     pl = PanelLasso(Ab, 2, nrhs=k, device=0)
     pl.set_tuning("d_split", d_split)
     out = []
-    # 3: the staggered four-phase form (k = 128; others fall back to 2); 4: pass 2 on 512-row tiles
-    # (k = 128; pass 1 and other k: the form of 1)
-    for v in (0, 1, 2, 3, 4):
+    for v in (0, 1, 2, 3):            # 3: the staggered four-phase form (k = 128; others fall back to 2)
         pl.set_tuning("interleave", v)
         out.append(pl.run(B, mu, 12)["x"])
     for o in out[1:]:
@@ -128,20 +126,6 @@ def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
         pl.set_tuning("no_such_knob", 1)
     with pytest.raises(Exception):
         pl.set_tuning("d_split", 3)
-
-
-@pytest.mark.parametrize("kchunks,d_split,blocks", [(16, 2, 1), (4, 2, 1), (8, 1, 1), (2, 2, 3)])
-def test_panel_wide_pass2_is_bitwise_neutral(kchunks, d_split, blocks):
-    """interleave2 4 (pass 2 on 512-row tiles, RHS halves of the direction refilled half a stage
-    ahead) against the 256-row form at the same kchunks: the same slab, bitwise."""
-    Ab, B, mu = instance(1024, 4096 if blocks == 1 else 1024 * blocks, 128, seed=31)
-    pl = PanelLasso(Ab, blocks, nrhs=128, device=0, kchunks=kchunks)
-    pl.set_tuning("d_split", d_split)
-    pl.set_tuning("interleave2", 1)
-    a = pl.run(B, mu, 16)["x"]
-    pl.set_tuning("interleave2", 4)
-    b = pl.run(B, mu, 16)["x"]
-    np.testing.assert_array_equal(a, b)
 
 
 @pytest.mark.parametrize("blocks,d_split", [(1, 2), (2, 2), (2, 1)])
