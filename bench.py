@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
 """Benchmark: ISTA (block best-response) iterations/s on dense fp32 A, 1..8 MI355X.
 
-One "step" = one iteration of the hot path (reference lasso.py:102-157): a
-full pass over the active block of A for A^T r, the shrink, a second pass for
-A D, the line search and the update -- all on the device, inputs resident in
-HBM before the timed region.
+One "step" = one iteration of the hot path (reference lasso.py:102-157: the
+shrink, s23 = A D, the exact line search, the x / Ax update and the next
+gradient), all on the device, inputs resident in HBM before the timed region.
+With one feature block (every default workload) the iteration streams A ONCE:
+k_onepass forms s23 = A D and U = A^T s23 from one pass and the gradient is
+carried as g += gamma U, with an exact g = A^T r every 256 iterations (folded
+into the rate at its amortised cost, below); with several feature blocks, or
+across column shards, it is the reference's two passes (A^T r, then A D).
 
   N = 1 : BASELINE configs[1]  m=8192 n=65536 fp32 A, one feature block.
   N > 1 : BASELINE configs[2]  m=8192 n=65536*N (n = 524288 at N = 8), weak scaling:
@@ -18,8 +22,11 @@ HBM before the timed region.
           iteration and one all-reduce of m + 2 + N fp64 on the residual side).
           The work unit is one "block-iteration" = one iteration's worth of an
           8192 x 65536 fp32 matrix (the whole configs[1] matrix), so value = N x
-          global iterations/s.  A strong-scaling measurement (the fixed 8192 x 65536
-          matrix split N ways the same way) is reported beside it under "strong".
+          global iterations/s.  Beside it, from the same run: "strong" (the fixed
+          8192 x 65536 matrix split N ways by rows), "columns" (the reference's
+          column split of the same weak problem, and its strong form), each with
+          its per-rank all-reduce times, and "n1_same_run" (rank 0 alone on the
+          N = 1 problem, with the efficiencies of the legs against it).
   --config 2: configs[2]'s own problem (m=8192 n=524288) split over the N GPUs
           (strong scaling; at N = 1 the whole 16 GiB matrix on one GPU).
   --config 3 / 4: configs[3] (1048576 x 4096 fp32) / configs[4] (k = 128
@@ -193,11 +200,20 @@ class Ctx:
         # rehearsal of the N > 1 code path on a one-GPU box (every rank on this device;
         # numbers meaningless): BPGL_BENCH_DEVICE=0.  RCCL refuses two ranks of one node on
         # one GPU, so each rank claims its own host id and the ranks talk over loopback sockets.
+        # BPGL_BENCH_CU_PARTITION=1 with it: every rank's solver stream gets a disjoint,
+        # XCD-symmetric 1/N of the CUs (distributed.xcd_symmetric_cu_mask), so each rank's
+        # persistent one-pass grid is sized to its CUs and the default N > 1 path runs as
+        # designed (the ranks still share one GPU's HBM: rates are not N-GPU rates).
+        self.cu_mask = None
         if os.environ.get("BPGL_BENCH_DEVICE"):
             self.local = int(os.environ["BPGL_BENCH_DEVICE"])
             os.environ["NCCL_HOSTID"] = f"bpgl-rehearsal-{self.rank}"
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
             os.environ.setdefault("NCCL_IB_DISABLE", "1")
+            if os.environ.get("BPGL_BENCH_CU_PARTITION") == "1" and self.world > 1:
+                from convex_optimization_amd.distributed import xcd_symmetric_cu_mask
+                cus = torch.cuda.get_device_properties(self.local).multi_processor_count
+                self.cu_mask = xcd_symmetric_cu_mask(self.rank, self.world, cus)
         self.dist = dist
         if self.world > 1:
             dist.init_process_group("gloo")
@@ -238,7 +254,7 @@ def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, sha
         idx = torch.cat([torch.arange(s, e) for s, e in bounds]).to(f"cuda:{ctx.local}")
         col_range = idx
     gc, b, mu, _ = device_instance(m, n_total, 0.4, block, TYPE=type_name, seed=seed, device=ctx.local,
-                                   comm=comm, col_range=col_range, row_range=row_range)
+                                   comm=comm, col_range=col_range, row_range=row_range, cu_mask=ctx.cu_mask)
     torch.cuda.synchronize()
     return gc, b, mu
 
@@ -263,7 +279,10 @@ def median(v):
 
 def measure(ctx, args, m, n_total):
     """W warm-up iterations, an eager window with per-kernel HIP events (max(K, 512) iterations),
-    then `windows` graph windows of exactly K iterations (see the module docstring)."""
+    then `windows` graph windows of exactly K iterations (see the module docstring).  A window is
+    valid when it ran the iteration the solve started with (one pass or two) and lost no
+    iterations; if a one-pass launch failed before the windows (every window then runs on the
+    two-pass kernels), the solver is reset and the whole sequence measured once more."""
     import torch
     gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard)
     gc.set_tuning("fused", args.fused)
@@ -280,39 +299,87 @@ def measure(ctx, args, m, n_total):
         gc.stream.synchronize()
         torch.cuda.synchronize()
 
-    gc.solver_reset(b, mu, use_graph=True)
-    gc.solver_step(args.warmup)
-    sync()
-    # eager window: kernel averages (events on the solver stream) + clock ramp
-    n_ev = max(args.steps, args.ramp)
-    gc.set_kernel_timing(True)
-    r0 = gc.solver_stat("refreshes")
-    el_ev = timed_window(ctx, sync, gc.solver_step, n_ev)
-    n_ref_ev = gc.solver_stat("refreshes") - r0
-    times, samples = gc.kernel_times()
-    gc.set_kernel_timing(False)
-    refresh_ms = times["refresh"] * samples / n_ref_ev if n_ref_ev else 0.0
-    refresh_ms = ctx.max(refresh_ms)
-    st = gc.solver_status()   # completes any iteration a failed one-pass launch lost (outside the windows)
-    period = gc.solver_stat("refresh_period")
-    # graph windows; after each, the status call (outside the window) would re-run iterations a
-    # failed one-pass launch lost -- such a window did not do its K iterations and is dropped
-    wins = []
-    for _ in range(args.windows):
+    for attempt in range(2):
+        gc.solver_reset(b, mu, use_graph=True)
+        op0 = gc.solver_stat("onepass")
+        gc.solver_step(args.warmup)
+        sync()
+        # eager window: kernel averages (events on the solver stream) + clock ramp
+        n_ev = max(args.steps, args.ramp)
+        gc.set_kernel_timing(True)
         r0 = gc.solver_stat("refreshes")
-        rec0 = gc.solver_stat("fallbacks")
-        el = timed_window(ctx, sync, gc.solver_step, args.steps)
-        n_ref = ctx.max(gc.solver_stat("refreshes") - r0)
-        st = gc.solver_status()
-        lost = ctx.max(gc.solver_stat("fallbacks") - rec0) > 0
-        adj = el - n_ref * refresh_ms * 1e-3 + (args.steps / period * refresh_ms * 1e-3 if period else 0.0)
-        wins.append({"s": el, "refreshes": int(n_ref), "s_amortised": adj, "lost_iterations": bool(lost)})
-    if all(w["lost_iterations"] for w in wins):
-        raise SystemExit("every timed window lost one-pass iterations (another process holds CUs?)")
+        el_ev = timed_window(ctx, sync, gc.solver_step, n_ev)
+        n_ref_ev = gc.solver_stat("refreshes") - r0
+        times, samples = gc.kernel_times()
+        gc.set_kernel_timing(False)
+        refresh_ms = times["refresh"] * samples / n_ref_ev if n_ref_ev else 0.0
+        refresh_ms = ctx.max(refresh_ms)
+        st = gc.solver_status()   # completes any iteration a failed one-pass launch lost (outside the windows)
+        eager_op = int(min(ctx.gather(gc.solver_stat("onepass"))))
+        period = gc.solver_stat("refresh_period")
+        # graph windows; after each, the status call (outside the window) re-runs iterations a
+        # failed one-pass launch lost -- such a window did not do its K iterations, and a window
+        # after a fallback runs the two-pass kernels: neither counts toward the median
+        wins = []
+        for _ in range(args.windows):
+            r0 = gc.solver_stat("refreshes")
+            rec0 = gc.solver_stat("fallbacks")
+            el = timed_window(ctx, sync, gc.solver_step, args.steps)
+            n_ref = ctx.max(gc.solver_stat("refreshes") - r0)
+            st = gc.solver_status()
+            lost = ctx.max(gc.solver_stat("fallbacks") - rec0) > 0
+            op = int(min(ctx.gather(gc.solver_stat("onepass"))))
+            adj = el - n_ref * refresh_ms * 1e-3 + (args.steps / period * refresh_ms * 1e-3 if period and op else 0.0)
+            wins.append({"s": el, "refreshes": int(n_ref), "s_amortised": adj, "lost_iterations": bool(lost),
+                         "onepass": op, "valid": (not lost) and op == op0})
+        if any(w["valid"] for w in wins) and eager_op == op0:
+            break
+        if attempt == 1:
+            raise SystemExit("every timed window lost one-pass iterations or fell back to two passes "
+                             "(another process holds CUs?)")
     assert st["iters"] == args.warmup + n_ev + args.windows * args.steps or st["stopped"], st
     return dict(gc=gc, windows=wins, el_events=el_ev, n_events=n_ev, kernel_ms=times, samples=samples, status=st,
                 refresh_ms=refresh_ms, refresh_period=period, w_local=gc.MAT_WIDTH, m_local=gc.MAT_HEIGHT,
-                b=b, mu=mu, fallbacks=gc.solver_stat("fallbacks"), onepass=gc.solver_stat("onepass"))
+                b=b, mu=mu, fallbacks=gc.solver_stat("fallbacks"), onepass=gc.solver_stat("onepass"),
+                attempts=attempt + 1, cus=gc.solver_stat("cus"))
+
+
+def window_rate(res, K):
+    """iterations/s of the median valid window (the refresh folded in), and that window's raw time"""
+    ok = [x for x in res["windows"] if x["valid"]]
+    return K / median([x["s_amortised"] for x in ok]), median([x["s"] for x in ok]) / K
+
+
+class SoloCtx:
+    """rank 0 alone (no collectives): the N = 1 reference leg inside an N > 1 run"""
+
+    def __init__(self, ctx):
+        self.rank, self.world, self.local, self.cu_mask, self.dist = 0, 1, ctx.local, None, None
+
+    def barrier(self):
+        pass
+
+    def max(self, v):
+        return v
+
+    def gather(self, v):
+        return [float(v)]
+
+
+def leg_summary(ctx, res, K, G, weak):
+    """a secondary measurement of an N > 1 run (its own key in the JSON line)"""
+    v, raw = window_rate(res, K)
+    kms = res["kernel_ms"]
+    return {"value": v * G if weak else v,
+            "unit": "block-iters/s" if weak else "iters/s",
+            "ms_per_step": 1e3 / v,
+            "ms_per_step_raw_median": raw * 1e3,
+            "config": f"{res['m_local']} rows x {res['w_local']} cols per GPU",
+            "split": res["gc"].shard if G > 1 else "none",
+            "iteration": "one pass over A" if kms.get("onepass", 0.0) > 0 else "two passes over A",
+            "kernel_avg_ms": kms,
+            "allreduce_ms_per_rank": ctx.gather(kms.get("allreduce", 0.0)),
+            "onepass_fallbacks": res["fallbacks"], "cus_per_rank": res["cus"]}
 
 
 def host_cores():
@@ -657,7 +724,7 @@ def main():
     w, ml = res["w_local"], res["m_local"]
     rows = res["gc"].shard == "rows"
     K = args.steps
-    ok = [x for x in res["windows"] if not x["lost_iterations"]]
+    ok = [x for x in res["windows"] if x["valid"]]
     el_med = median([x["s_amortised"] for x in ok])
     el_raw = median([x["s"] for x in ok])
     iters_s = K / el_med
@@ -754,19 +821,57 @@ def main():
         note = "" if G == 1 else f" (rank 0's share of the {G}-GPU problem: {ml} x {w})"
         out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds, cores, cpu_info, note)
         out["cpu_baseline"]["pool_configs0"] = pool
-    if G > 1 and not args.no_strong and not args.strong_total:
-        del res
-        torch.cuda.empty_cache()
-        a2 = argparse.Namespace(**vars(args))
-        strong = measure(ctx, a2, m, args.n_per_gpu)
-        so = [x for x in strong["windows"] if not x["lost_iterations"]]
-        out["strong"] = {"value": K / median([x["s_amortised"] for x in so]), "unit": "iters/s",
-                         "config": f"m={m} n={args.n_per_gpu} split {G} ways ({strong['m_local']} rows x "
-                                   f"{strong['w_local']} cols per GPU)",
-                         "kernel_avg_ms": strong["kernel_ms"],
-                         "allreduce_ms_per_rank": ctx.gather(strong["kernel_ms"].get("allreduce", 0.0))}
-        res = strong
-    if G == 1 and args.type == "float":
+    out["config"]["measure_attempts"] = res["attempts"]
+    out["config"]["cus_per_rank"] = res["cus"]
+    if G > 1 and not args.no_strong:
+        # the other legs of one SCALE run: the same fixed matrix split N
+        # ways (strong), the reference's column split (two passes, all-reduce of m + 2 + N on the
+        # residual side, cpu_calculation.py:23-27) beside the row split, and rank 0 alone on the
+        # N = 1 problem -- so the split choice and both efficiencies come from one run
+        def fresh():   # drop the previous leg's context, A and communicator before the next
+            nonlocal res
+            res = None
+            import gc as _gc
+            _gc.collect()
+            torch.cuda.empty_cache()
+        if not args.strong_total:
+            fresh()
+            res = measure(ctx, argparse.Namespace(**vars(args)), m, args.n_per_gpu)
+            out["strong"] = leg_summary(ctx, res, K, G, False)
+            out["strong"]["config"] = f"m={m} n={args.n_per_gpu} split {G} ways ({out['strong']['config']})"
+        if args.block == 1 and rows:
+            a2 = argparse.Namespace(**vars(args))
+            a2.shard = "columns"
+            fresh()
+            res = measure(ctx, a2, m, n_total)
+            out["columns"] = leg_summary(ctx, res, K, G, weak)
+            out["columns"]["config"] = f"m={m} n={n_total} column-sharded ({out['columns']['config']})"
+            if not args.strong_total:
+                fresh()
+                res = measure(ctx, a2, m, args.n_per_gpu)
+                out["columns"]["strong"] = leg_summary(ctx, res, K, G, False)
+        if not args.strong_total:
+            fresh()
+            ctx.barrier()
+            n1 = None
+            if ctx.rank == 0:
+                a3 = argparse.Namespace(**vars(args))
+                a3.comm = False
+                res = measure(SoloCtx(ctx), a3, m, args.n_per_gpu)
+                n1 = window_rate(res, K)[0]
+            ctx.barrier()
+            if ctx.rank == 0:
+                o = {"value": n1, "unit": "iters/s",
+                     "config": f"m={m} n={args.n_per_gpu} on rank 0's GPU alone (no communicator), same run",
+                     "efficiency_weak_rows": out["value"] / (G * n1)}
+                if "strong" in out:
+                    o["speedup_strong_rows"] = out["strong"]["value"] / n1
+                if "columns" in out:
+                    o["efficiency_weak_columns"] = out["columns"]["value"] / (G * n1)
+                    if "strong" in out["columns"]:
+                        o["speedup_strong_columns"] = out["columns"]["strong"]["value"] / n1
+                out["n1_same_run"] = o
+    if G == 1 and args.type == "float" and res is not None:
         out["config"]["vendor_gemv_yardstick"] = vendor_yardstick(res["gc"])
         out["config"]["vendor_iteration_yardstick"] = vendor_iteration_yardstick(res["gc"], res["b"], res["mu"])
     if ctx.rank == 0:

@@ -39,6 +39,8 @@ _pp = ctypes.POINTER(ctypes.c_void_p)
 _SIGS = {
     "bpgl_last_error": (ctypes.c_char_p, []),
     "bpgl_version": (_int, []),
+    "bpgl_stream_create": (_int, [_int, ctypes.POINTER(ctypes.c_uint32), _i32, _pp]),
+    "bpgl_stream_destroy": (_int, [_p]),
     "bpgl_create": (_int, [_pp, _int, _int, _i64, _i64, _i32, _p]),
     "bpgl_destroy": (None, [_p]),
     "bpgl_stream": (_p, [_p]),

@@ -45,6 +45,29 @@ constexpr int kTimedKinds = 9;   // + 8: the exact-gradient refresh of the one-p
 constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
+
+constexpr int kMaskWords = 32;   // CU mask words queried (1024 CUs)
+
+int popcount_mask(const uint32_t* mask, int words, int cus) {
+    int n = 0;
+    for (int i = 0; i < words; ++i) {
+        uint32_t v = mask[i];
+        if (32 * i >= cus) break;
+        if (32 * (i + 1) > cus) v &= (1u << (cus - 32 * i)) - 1u;
+        n += __builtin_popcount(v);
+    }
+    return n;
+}
+
+// CUs a stream may use (its CU mask, hipExtStreamGetCUMask), 0 if unknown
+int stream_cus(hipStream_t s, int dev_cus) {
+    uint32_t mask[kMaskWords] = {};
+    if (hipExtStreamGetCUMask(s, kMaskWords, mask) != hipSuccess) {
+        (void)hipGetLastError();   // not sticky: later launch checks read hipGetLastError
+        return 0;
+    }
+    return popcount_mask(mask, kMaskWords, dev_cus);
+}
 }  // namespace
 
 struct bpgl_ctx {
@@ -82,7 +105,9 @@ struct bpgl_ctx {
     int nt_loads = 1;
     int tail_permille = 120;
     // one-pass iteration (bpgl_onepass.h)
-    int cus = 256;
+    int cus = 256;             // CUs the persistent grid is sized for (the stream's CU mask, or "cus")
+    int dev_cus = 256;         // CUs of the device
+    bool cu_masked = false;    // the stream carries a CU mask narrower than the device
     int onepass = -1;          // tuning: -1 when eligible, 0 off, 1 required
     // exact g = A^T r every this many iterations (0: at reset only).  The recurrence's own drift is
     // below the trajectory's rounding sensitivity: after 1024 iterations at configs[1], x is within
@@ -741,6 +766,29 @@ extern "C" {
 const char* bpgl_last_error(void) { return bpgl_host::g_err.c_str(); }
 int bpgl_version(void) { return 100; }
 
+int bpgl_stream_create(int device, const uint32_t* cu_mask, int32_t mask_words, void** out) {
+    if (!out) return fail(BPGL_E_ARG, "out is null");
+    *out = nullptr;
+    if (cu_mask && mask_words <= 0) return fail(BPGL_E_ARG, "mask_words must be > 0");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    if (cu_mask) {
+        int dev_cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device));
+        if (popcount_mask(cu_mask, mask_words, dev_cus) == 0) return fail(BPGL_E_ARG, "the CU mask selects no CU");
+        HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask_words, cu_mask));
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    *out = (void*)s;
+    return 0;
+}
+
+int bpgl_stream_destroy(void* stream) {
+    if (stream) HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return 0;
+}
+
 int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_local, int32_t nblock,
                 void* hip_stream) {
     if (!out) return fail(BPGL_E_ARG, "out is null");
@@ -762,6 +810,7 @@ int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_lo
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         c->cus = cus;
+    c->dev_cus = c->cus;
     if (hip_stream) {
         c->stream = (hipStream_t)hip_stream;
     } else {
@@ -770,6 +819,14 @@ int bpgl_create(bpgl_ctx** out, int device, int a_dtype, int64_t m, int64_t n_lo
             return fail(BPGL_E_HIP, "hipStreamCreate failed");
         }
         c->own_stream = true;
+    }
+    {   // a CU-masked stream (bpgl_stream_create): the persistent one-pass grid is sized to the CUs
+        // the stream may use, so all of its blocks stay resident beside other masked streams
+        const int n = stream_cus(c->stream, c->dev_cus);
+        if (n > 0 && n < c->dev_cus) {
+            c->cus = n;
+            c->cu_masked = true;
+        }
     }
     int rate_khz = 0;
     if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && rate_khz > 0)
@@ -1136,6 +1193,9 @@ int bpgl_solver_stat(bpgl_ctx* c, const char* key, int64_t* value) {
     else if (!strcmp(key, "fallbacks")) *value = c->n_fallback;
     else if (!strcmp(key, "requested")) *value = c->req_t;
     else if (!strcmp(key, "enqueued")) *value = c->op_t;
+    else if (!strcmp(key, "cus")) *value = c->cus;
+    else if (!strcmp(key, "cu_masked")) *value = c->cu_masked ? 1 : 0;
+    else if (!strcmp(key, "onepass_grid")) *value = (int64_t)c->op_ngroups * c->op_SB;
     else return fail(BPGL_E_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1149,7 +1209,10 @@ int bpgl_iterate(bpgl_ctx* c, int64_t n_iter, const int32_t* order, double mu, c
                                 1)))
         return rc;
     if ((rc = bpgl_solver_step(c, n_iter))) return rc;
-    if (iters_done) return bpgl_solver_status(c, iters_done, nullptr, nullptr, nullptr, nullptr);
+    // always: the status call synchronises and re-runs iterations a failed one-pass launch lost
+    int64_t done = 0;
+    if ((rc = bpgl_solver_status(c, &done, nullptr, nullptr, nullptr, nullptr))) return rc;
+    if (iters_done) *iters_done = done;
     return 0;
 }
 
@@ -1223,6 +1286,13 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->op.fail_at = c->op_fail_at;
         drop_graphs(c);
         c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "cus")) {   // size the persistent grids for this many CUs (the layout depends on it)
+        if (c->bound) return fail(BPGL_E_STATE, "\"cus\" must be set before bpgl_bind (it sets the scratch layout)");
+        if (value < 1 || value > c->dev_cus) return fail(BPGL_E_ARG, "cus must be in [1, %d]", c->dev_cus);
+        c->cus = (int)value;
+        geometry(c);
         return 0;
     }
     if (!strcmp(key, "onepass_refresh")) {

@@ -18,8 +18,7 @@ using namespace bpgl_host;
 // ===========================================================================
 // panel path (k right-hand sides, bf16 A, MFMA): BASELINE configs[4]
 // ===========================================================================
-constexpr int kPanelKinds = 5;
-   // pass1, pass2, reduce, step, update
+constexpr int kPanelKinds = 5;   // pass1, pass2, reduce, step, update
 
 struct bpgl_panel {
     int device = 0;

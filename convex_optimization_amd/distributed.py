@@ -76,6 +76,29 @@ def shard_rows(A, rank, nranks):
     return A[s:e].contiguous()
 
 
+def xcd_symmetric_cu_mask(rank, nranks, cus=256):
+    """CU mask words (bit i = CU i) giving rank `rank` of `nranks` (1, 2 or 4) processes that share
+    one GPU a disjoint 1/nranks of its CUs, the same number on every XCD.
+
+    The mask is built so that it does not depend on how the driver maps mask bits to XCDs: every
+    32-bit word is split into four bytes and a rank takes whole bytes (rank k of 2: bytes k and
+    k + 2; of 4: byte k).  A byte holds 8 consecutive bits, one of each residue mod 8 (bits
+    interleaved over the 8 XCDs) and a word is one XCD's 32 CUs (bits in XCD-sized runs), so
+    either way every XCD gets 32/nranks of the rank's CUs.  The one-pass grid is persistent: an XCD
+    left without CUs would never run its share of blocks."""
+    if nranks not in (1, 2, 4):
+        raise ValueError("CU partitions are built for 1, 2 or 4 ranks per GPU")
+    if not 0 <= rank < nranks:
+        raise ValueError(f"rank {rank} out of range for {nranks}")
+    if cus % 32:
+        raise ValueError("the device's CU count must be a multiple of 32")
+    per = 4 // nranks
+    word = 0
+    for k in range(per):
+        word |= 0xFF << (8 * (rank + k * nranks))
+    return [word] * (cus // 32)
+
+
 def row_exchange_layout(wp):
     """Offsets in the row-shard all-reduce buffer (SUM over ranks); `failed` carries each rank's
     one-pass failure flag (a nonzero sum makes every rank skip the iteration)."""

@@ -20,9 +20,13 @@ semantics (gpu_calculation.py:141-292) so the reference drivers
     crosses PCIe.
 
 New: ``run`` -- the whole solver loop resident on the
-device (one fused iteration = colpass / shrink / rowpass / rowreduce / step /
-update, captured once as a hipGraph), returning x, which the reference's
-drivers never did (lasso.py:167-169, :609).
+device, captured once as hipGraphs of 1 and 8 iterations, returning x, which
+the reference's drivers never did (lasso.py:167-169, :609).  With one feature
+block an iteration is ``k_onepass`` (A read once: s23 = A D and U = A^T s23,
+the line search by its last row group) + ``k_onepass_tail`` (x, Ax, r,
+g += gamma U and the next shrink), with an exact g = A^T r every 256
+iterations; with several blocks (or ``onepass`` = 0) it is the two-pass
+sequence colpass / shrink / rowpass / rowreduce (+ line search) / update.
 
 Every compute call goes through libbpgl.so (``_native``); there is no
 alternative path.  Multi-GPU: pass ``comm=`` (see ``distributed.RankComm``);
@@ -52,16 +56,39 @@ def _resolve_device(A, device):
     return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())
 
 
+_MASKED_STREAMS = {}
+
+
+def _masked_stream(device, mask):
+    """The CU-masked stream of (device, mask), created once per process by libbpgl
+    (bpgl_stream_create) and kept for the life of the process: torch's caching allocator keys the
+    blocks of every tensor allocated on a stream by that stream, so the stream must outlive them
+    (destroying it with the context crashed the allocator at exit)."""
+    key = (device.index, tuple(mask))
+    st = _MASKED_STREAMS.get(key)
+    if st is None:
+        words = (ctypes.c_uint32 * len(mask))(*mask)
+        sp = ctypes.c_void_p()
+        N.check(N.lib().bpgl_stream_create(device.index, words, len(mask), ctypes.byref(sp)), "bpgl_stream_create")
+        st = torch.cuda.ExternalStream(sp.value, device=device)
+        _MASKED_STREAMS[key] = st
+    return st
+
+
 class GPU_Calculation:
     T_WIDTH_TRANS = 64
     T_WIDTH = 64
     T_HEIGHT = 512
     TYPE = 'double'
 
-    def __init__(self, A, Block, device=None, comm=None, shard="columns"):
+    def __init__(self, A, Block, device=None, comm=None, shard="columns", cu_mask=None):
+        """``cu_mask``: optional sequence of uint32 words (bit i = CU i) restricting the solver's
+        stream to those CUs (several ranks sharing one GPU; see
+        ``distributed.xcd_symmetric_cu_mask``); the persistent one-pass grid is then sized to them."""
         if shard not in ("columns", "rows"):
             raise ValueError("shard must be 'columns' or 'rows'")
         self.shard = shard
+        self._cu_mask = None if cu_mask is None else [int(w) & 0xFFFFFFFF for w in cu_mask]
         self.Block = int(Block)
         self.MAT_WIDTH_ALL = int(A.shape[1])
         self.device = _resolve_device(A, device)
@@ -87,7 +114,10 @@ class GPU_Calculation:
         H, W, Wp, B = self.MAT_HEIGHT, self.MAT_WIDTH, self.MAT_WIDTH_PAD, self.Block
         tdt = N.TORCH_DTYPE[self._dt]
         torch.cuda.set_device(self.device)
-        self.stream = torch.cuda.Stream(device=self.device)
+        if self._cu_mask is not None:
+            self.stream = _masked_stream(self.device, self._cu_mask)
+        else:
+            self.stream = torch.cuda.Stream(device=self.device)
         ctx = ctypes.c_void_p()
         N.check(L.bpgl_create(ctypes.byref(ctx), self.device.index, self._dt, H, B * W, B,
                               ctypes.c_void_p(self.stream.cuda_stream)), "bpgl_create")
@@ -273,8 +303,10 @@ class GPU_Calculation:
         return v.value
 
     def solver_x(self):
-        """Current iterate as a host ndarray (K_local,) in the reference's block order."""
-        self.stream.synchronize()
+        """Current iterate as a host ndarray (K_local,) in the reference's block order.  Goes
+        through solver_status first, so iterations a failed one-pass launch lost are re-run
+        before x is read (RCCL row shards: every rank must call it, as solver_status)."""
+        self.solver_status()
         return self._x[:, :self.MAT_WIDTH].reshape(-1).cpu().numpy().copy()
 
     def _ctx_residual(self):
@@ -284,10 +316,12 @@ class GPU_Calculation:
         return self._scratch[off:off + self.MAT_HEIGHT]
 
     def solver_x_device(self):
+        """Device view of x; call solver_status() first (it re-runs lost one-pass iterations)."""
         return self._x[:, :self.MAT_WIDTH]
 
     def solver_records(self):
-        self.stream.synchronize()
+        """(err_iter, time_iter) host copies, after solver_status (as solver_x)."""
+        self.solver_status()
         if self._err_iter is None:
             return None, None
         return self._err_iter.cpu().numpy().copy(), self._time_iter.cpu().numpy().copy()

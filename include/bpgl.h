@@ -57,6 +57,21 @@ const char* bpgl_last_error(void);
 int bpgl_version(void);
 
 /*
+ * A HIP stream for a context, optionally restricted to a set of CUs
+ * (hipExtStreamCreateWithCUMask; bit i of cu_mask[i / 32] enables CU i).  Several
+ * processes (ranks) sharing one GPU each get disjoint CUs this way, so the
+ * persistent one-pass grid of every rank stays resident beside the others.
+ * bpgl_create sizes that grid to the CUs its stream may use (hipExtStreamGetCUMask;
+ * the tuning key "cus" overrides it before bpgl_bind).  The mask should give
+ * every XCD the same number of CUs: the python helper
+ * distributed.xcd_symmetric_cu_mask builds one.  cu_mask NULL: an unrestricted
+ * non-blocking stream.  No reference counterpart (pycuda used one context and
+ * the default stream, gpu_calculation.py:4).
+ */
+int bpgl_stream_create(int device, const uint32_t* cu_mask, int32_t mask_words, void** stream_out);
+int bpgl_stream_destroy(void* stream);
+
+/*
  * Create a context for an m x n_local matrix split into nblock feature blocks.
  * Replaces GPU_Calculation.__init__ / init_cpu_array (gpu_calculation.py:148-220):
  * grid sizes and scratch needs are derived here instead of per-call numpy.
@@ -181,12 +196,16 @@ double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
  *   which stay in use for the rest of the solve (RCCL row shards: the two-pass
  *   row iteration, two passes over the local rows and two all-reduces per
  *   iteration; every rank switches at the same iteration, so RCCL row-shard
- *   ranks must all call it at the same point).
+ *   ranks must all call it at the same point: the recovery is collective --
+ *   it enqueues all-reduces, so every rank must enter bpgl_solver_status
+ *   concurrently, one process or thread per rank).
  * bpgl_solver_stat: counters since the last reset -- "onepass" (1 while the
  *   one-pass iteration is in use), "refresh_period" (iterations between
  *   exact-gradient refreshes, 0 = none), "refreshes" (exact-gradient refreshes
  *   enqueued), "fallbacks" (recoveries above), "requested"
- *   (iterations asked of bpgl_solver_step), "enqueued".
+ *   (iterations asked of bpgl_solver_step), "enqueued", "cus" (CUs the
+ *   persistent grid is sized for), "cu_masked" (1: narrower than the device,
+ *   from the stream's CU mask), "onepass_grid" (its blocks).
  * bpgl_solver_residual: device pointer of the residual s11 = sum_k Ax_k - b (m).
  */
 int bpgl_solver_reset(bpgl_ctx* ctx, const double* b, double mu, double* x,
@@ -200,8 +219,9 @@ int bpgl_solver_stat(bpgl_ctx* ctx, const char* key, int64_t* value);
 const double* bpgl_solver_residual(bpgl_ctx* ctx);
 
 /*
- * One-call form: reset, run n_iter iterations, wait, report.  The survey's
- * bpgl_iterate.  iters_done may be NULL.
+ * One-call form: reset, run n_iter iterations, wait (bpgl_solver_status, so lost
+ * one-pass iterations are re-run whether or not iters_done is given), report.
+ * The survey's bpgl_iterate.  iters_done may be NULL.
  */
 int bpgl_iterate(bpgl_ctx* ctx, int64_t n_iter, const int32_t* order, double mu,
                  const double* b, double* x, double* err_iter, double* time_iter,
@@ -247,6 +267,9 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   bytes, x within 2e-7 (1 rank) to 1.5e-6 (8 ranks) of the fp64 exchange.
  *   "onepass_fail_at" (test hook, default -1): the one-pass launch of iteration t
  *   reports a row hand-off failure once (exercises the recovery above).
+ *   "cus" (before bpgl_bind only; default: the stream's CU mask, else the device):
+ *   the CU count the persistent one-pass grid (row groups x segment blocks) is
+ *   sized for.
  * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the
  * number of (row chunk x column segment) tiles per two-pass launch (default
  * 1024 for fp32 A, 512 for fp64 / bf16). */

@@ -1,12 +1,20 @@
-"""Worker of tests/test_rccl_ranks.py: one rank of a two-rank RCCL solve on ONE GPU.
+"""Worker of tests/test_rccl_ranks.py: one rank of a multi-rank RCCL solve on ONE GPU.
 
-Launched by torch.distributed.run (RANK / WORLD_SIZE / MASTER_* in the environment).  Both
-ranks use device 0; each rank announces its own NCCL_HOSTID, so RCCL treats them as two hosts
-and moves the all-reduce over loopback sockets (the same trick as tools/rehearse_n2.sh).  The
-data path is the product's: libbpgl's communicator, the all-reduce issued on the solver stream.
+Launched by torch.distributed.run (RANK / WORLD_SIZE / MASTER_* in the environment).  Every
+rank uses device 0; each rank announces its own NCCL_HOSTID, so RCCL treats them as separate
+hosts and moves the all-reduce over loopback sockets (the same trick as tools/rehearse_n2.sh).
+The data path is the product's: libbpgl's communicator, the all-reduce issued on the solver
+stream.
 
-usage: rccl_ranks_worker.py CASE SHARD OUTDIR   (SHARD: columns | rows)
+usage: rccl_ranks_worker.py CASE SHARD OUTDIR [--cumask] [--fail-rank R --fail-at T]
+  SHARD: columns | rows
+  --cumask: the rank's solver stream gets a disjoint, XCD-symmetric 1/WORLD_SIZE of the CUs
+            (distributed.xcd_symmetric_cu_mask), so each rank's persistent one-pass grid is
+            sized to its CUs and stays resident beside the other ranks' kernels
+  --fail-rank / --fail-at: rank R's one-pass launch of iteration T reports a hand-off failure
+            (tuning key "onepass_fail_at"), exercising the collective recovery
 """
+import argparse
 import os
 import sys
 
@@ -15,7 +23,14 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    case, shard, outdir = sys.argv[1], sys.argv[2], sys.argv[3]
+    ap = argparse.ArgumentParser()
+    ap.add_argument("case")
+    ap.add_argument("shard")
+    ap.add_argument("outdir")
+    ap.add_argument("--cumask", action="store_true")
+    ap.add_argument("--fail-rank", type=int, default=-1)
+    ap.add_argument("--fail-at", type=int, default=-1)
+    a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ["NCCL_HOSTID"] = f"bpgl-test-rank{rank}"   # before the communicator is created
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
@@ -30,31 +45,43 @@ def main():
 
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
-    fx = dict(np.load(os.path.join(ROOT, "tests", "golden", case + ".npz")))
+    fx = dict(np.load(os.path.join(ROOT, "tests", "golden", a.case + ".npz")))
     A = oracle.fixture_A(fx)
     block, iters = int(fx["BLOCK"]), int(fx["ITER_MAX"])
     eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
     b = np.asarray(fx["b"]).reshape(-1)
     GC = type("GC_float", (GPU_Calculation,), {"TYPE": "float"})
     comm = D.RankComm(rank, world)
-    if shard == "rows":
+    mask = None
+    if a.cumask:
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        mask = D.xcd_symmetric_cu_mask(rank, world, cus)
+    if a.shard == "rows":
         s, e = D.row_bounds(A.shape[0], rank, world)
-        gc = GC(D.shard_rows(A, rank, world), 1, device=0, comm=comm, shard="rows")
+        gc = GC(D.shard_rows(A, rank, world), 1, device=0, comm=comm, shard="rows", cu_mask=mask)
         b_local = b[s:e]
     else:
-        gc = GC(D.shard_columns(A, block, rank, world), block, device=0, comm=comm)
+        gc = GC(D.shard_columns(A, block, rank, world), block, device=0, comm=comm, cu_mask=mask)
         b_local = b
-    out = {}
+    out = {"cus": np.int64(gc.solver_stat("cus")), "cu_masked": np.int64(gc.solver_stat("cu_masked")),
+           "onepass_grid": np.int64(gc.solver_stat("onepass_grid"))}
     for graph in (True, False):
+        if rank == a.fail_rank and a.fail_at >= 0:
+            gc.set_tuning("onepass_fail_at", a.fail_at)
+        # every rank's set-up is finished before any rank's solve starts (nothing else on the GPU)
+        torch.cuda.synchronize()
+        dist.barrier()
         res = gc.run(b_local, float(fx["mu"]), iters, err_bound=eb, record=True, use_graph=graph)
         tag = "graph" if graph else "eager"
         out[f"x_{tag}"] = np.asarray(res["x"]).reshape(-1)
         out[f"err_{tag}"] = np.asarray(res["err_iter"])
         out[f"t_last_{tag}"] = np.int64(res["t_last"])
         out[f"stopped_{tag}"] = np.bool_(res["stopped"])
+        out[f"fallbacks_{tag}"] = np.int64(gc.solver_stat("fallbacks"))
+        out[f"onepass_{tag}"] = np.int64(gc.solver_stat("onepass"))
     out["diag"] = np.asarray(gc.diag_ATA).reshape(-1)
-    out["fallbacks"] = np.int64(gc.solver_stat("fallbacks"))
-    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
+    out["fallbacks"] = out["fallbacks_eager"]
+    np.savez(os.path.join(a.outdir, f"rank{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()
 

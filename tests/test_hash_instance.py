@@ -1,0 +1,42 @@
+"""The long-horizon fixtures' instance generator (tests/hash_instance.py): numpy and torch build the
+same A and b bit for bit, b is exact whatever the summation order, and every committed
+tests/golden/longrun_*.npz matches the generator at its stored sample points (CPU only)."""
+import glob
+import os
+
+import numpy as np
+
+import hash_instance as H
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_numpy_and_torch_agree_bitwise():
+    import torch
+    A = H.np_A(300, 1000)
+    b = H.np_b(A)
+    At = H.torch_A(300, 1000, "cpu")
+    assert torch.equal(At, torch.from_numpy(A))
+    assert np.array_equal(H.torch_b(At).numpy(), b)
+    rows, cols = H.sample_points(300, 1000, k=64)
+    assert np.array_equal(H.np_entries(rows, cols, 1000), A[rows, cols])
+
+
+def test_b_is_exact_in_any_order():
+    A = H.np_A(200, 4096)
+    x = H.np_x_true(4096)
+    b1 = H.np_b(A)
+    b2 = A.astype(np.float64)[:, ::-1] @ x[::-1] + H.np_e(200)
+    b3 = np.array([sum(float(a) * float(c) for a, c in zip(row[x != 0], x[x != 0])) for row in A[:5]])
+    assert np.array_equal(b1, b2)
+    assert np.array_equal(b1[:5] - H.np_e(200)[:5], b3)
+    assert 0.3 < np.count_nonzero(x) / x.size < 0.5
+
+
+def test_committed_fixtures_match_the_generator():
+    for path in sorted(glob.glob(os.path.join(GOLD, "longrun_*.npz"))):
+        fx = dict(np.load(path))
+        n = int(fx["n"])
+        assert np.array_equal(H.np_entries(fx["A_rows"], fx["A_cols"], n), fx["A_samples"]), path
+        assert int(fx["iters"]) >= 260 and fx["x"].shape == (n,) and np.isfinite(fx["x"]).all()
+        assert fx["err_iter"][-1] < fx["err_iter"][0]

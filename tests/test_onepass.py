@@ -266,3 +266,24 @@ def test_contention_with_a_concurrent_kernel():
     print(f"contention: fallbacks {gc.solver_stat('fallbacks')}, iters {st['iters']}")
     assert st["iters"] == 300
     assert rel(gc.solver_x(), clean["x"]) <= 1e-9, rel(gc.solver_x(), clean["x"])
+
+
+def test_iterate_recovers_without_iters_done(golden):
+    """bpgl_iterate (the one-call C entry point) always goes through bpgl_solver_status, so a
+    failed one-pass launch is re-run even when the caller passes iters_done = NULL (include/bpgl.h)"""
+    fx = golden("c1_b1_p1_f32in")
+    A = oracle.fixture_A(fx)
+    IT = int(fx["ITER_MAX"])
+    gc = make_cls("float")(A, 1, device=0)
+    gc.set_tuning("onepass", 1)
+    gc.set_tuning("onepass_fail_at", 37)
+    b = torch.tensor(np.asarray(fx["b"]).reshape(-1), dtype=torch.float64, device="cuda:0")
+    x = torch.zeros(gc.MAT_WIDTH_PAD, dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    with gc._on_stream():
+        N.check(N.lib().bpgl_iterate(gc._ctx, IT, None, float(fx["mu"]), N.ptr(b), N.ptr(x), None, None, -1.0,
+                                     None), "bpgl_iterate")
+    torch.cuda.synchronize()
+    assert gc.solver_stat("fallbacks") == 1
+    xr = x[:gc.MAT_WIDTH].cpu().numpy()
+    assert rel(xr, fx["x"]) <= 1e-9, rel(xr, fx["x"])

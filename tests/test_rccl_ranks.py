@@ -6,9 +6,13 @@ each announcing its own NCCL_HOSTID so RCCL accepts them (the all-reduce then cr
 sockets instead of xGMI: correctness only, no timing).  Unlike tests/test_rowshard.py, whose
 multi-rank cases sum the exchange buffers in the test, here the product's ncclAllReduce (inside
 the captured graph and eager) is the exchange.  Row shards on a shared GPU cannot keep the
-one-pass kernel's blocks co-resident, so they normally finish on the two-pass row iteration
- -- also the product path.  Tolerance: the reference fixture's x within
-1e-9 relative l2 (as every solver test), the ranks' x bit-identical (rows), graph = eager.
+one-pass kernel's blocks co-resident unless every rank's stream is confined to its own CUs:
+without CU masks they normally finish on the two-pass row iteration (DESIGN.md section 6.2);
+with XCD-symmetric CU masks (``--cumask``: 2 ranks x 128 CUs, 4 ranks x 64 CUs) each rank's
+persistent grid is sized to its CUs and the default N > 1 path -- one-pass row shards, k_onepass
++ k_onepass_fold + ncclAllReduce of [U | r.s23 | s23.s23 | failed] + k_onepass_tail -- runs
+end to end with no fallback.  Tolerance: the reference fixture's x within 1e-9 relative l2
+(as every solver test), the ranks' x bit-identical (rows), graph = eager.
 """
 import os
 import socket
@@ -32,12 +36,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(case, shard, tmp_path, world=2):
+def _launch(case, shard, tmp_path, world=2, extra=()):
     env = dict(os.environ)
     env.pop("NCCL_HOSTID", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "rccl_ranks_worker.py"), case, shard, str(tmp_path)]
+           os.path.join(ROOT, "tests", "rccl_ranks_worker.py"), case, shard, str(tmp_path), *extra]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     return [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
@@ -79,3 +83,42 @@ def test_two_rccl_ranks_row_shards(golden, world, tmp_path):
         T = int(fx["ITER_MAX"])
         np.testing.assert_allclose(out[0][f"err_{tag}"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
     print("row-shard fallbacks per rank:", [int(o["fallbacks"]) for o in out])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_row_shards_onepass_cu_masked(golden, world, tmp_path):
+    """The default N > 1 iteration (one-pass row shards over RCCL), every rank on its own CUs:
+    no rank falls back, x is bit-identical on every rank and matches the reference fixture
+    (c1_b1_p1_f32in: the reference's ClassLassoCPU on the fp32-rounded instance, lasso.py:102-157,
+    whose P-way shard sum lasso.py:107-126 is here a sum over ranks)."""
+    fx = golden("c1_b1_p1_f32in")
+    out = _launch("c1_b1_p1_f32in", "rows", tmp_path, world, ["--cumask"])
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    for o in out:
+        assert int(o["cus"]) == cus // world and int(o["cu_masked"]) == 1, (o["cus"], o["cu_masked"])
+        assert 0 < int(o["onepass_grid"]) <= cus // world
+    for tag in ("graph", "eager"):
+        for o in out:
+            assert int(o[f"onepass_{tag}"]) == 1 and int(o[f"fallbacks_{tag}"]) == 0, \
+                (tag, int(o[f"onepass_{tag}"]), int(o[f"fallbacks_{tag}"]))
+        for o in out[1:]:
+            np.testing.assert_array_equal(out[0][f"x_{tag}"], o[f"x_{tag}"])
+        assert rel(out[0][f"x_{tag}"], fx["x"]) <= 1e-9, (tag, rel(out[0][f"x_{tag}"], fx["x"]))
+        T = int(fx["ITER_MAX"])
+        np.testing.assert_allclose(out[0][f"err_{tag}"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
+    np.testing.assert_array_equal(out[0]["x_graph"], out[0]["x_eager"])
+
+
+def test_rccl_row_shards_collective_recovery(golden, tmp_path):
+    """One rank's one-pass launch fails (test hook on rank 0 only, inside an 8-iteration graph):
+    its flag rides the all-reduce, every rank skips the same iterations, and every rank's
+    bpgl_solver_status (entered concurrently, one process per rank) re-runs them on the two-pass
+    row iteration -- the same fallback count and the same x on every rank, the reference's x."""
+    fx = golden("c1_b1_p1_f32in")
+    out = _launch("c1_b1_p1_f32in", "rows", tmp_path, 2, ["--cumask", "--fail-rank", "0", "--fail-at", "37"])
+    for o in out:
+        assert int(o["fallbacks_graph"]) == 1 and int(o["onepass_graph"]) == 0
+        assert int(o["fallbacks_eager"]) == 0 and int(o["onepass_eager"]) == 1
+    for tag in ("graph", "eager"):
+        np.testing.assert_array_equal(out[0][f"x_{tag}"], out[1][f"x_{tag}"])
+        assert rel(out[0][f"x_{tag}"], fx["x"]) <= 1e-9, (tag, rel(out[0][f"x_{tag}"], fx["x"]))
