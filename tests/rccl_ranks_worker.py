@@ -11,8 +11,9 @@ usage: rccl_ranks_worker.py CASE SHARD OUTDIR [--cumask] [--fail-rank R --fail-a
   --cumask: the rank's solver stream gets a disjoint, XCD-symmetric 1/WORLD_SIZE of the CUs
             (distributed.xcd_symmetric_cu_mask), so each rank's persistent one-pass grid is
             sized to its CUs and stays resident beside the other ranks' kernels
-  --fail-rank / --fail-at: rank R's one-pass launch of iteration T reports a hand-off failure
-            (tuning key "onepass_fail_at"), exercising the collective recovery
+  --fail-rank / --fail-at: in the first (graph) solve, rank R's one-pass launch of iteration T
+            reports a hand-off failure (tuning key "onepass_fail_at"), exercising the collective
+            recovery; the second (eager) solve runs undisturbed
 """
 import argparse
 import os
@@ -66,7 +67,7 @@ def main():
     out = {"cus": np.int64(gc.solver_stat("cus")), "cu_masked": np.int64(gc.solver_stat("cu_masked")),
            "onepass_grid": np.int64(gc.solver_stat("onepass_grid"))}
     for graph in (True, False):
-        if rank == a.fail_rank and a.fail_at >= 0:
+        if graph and rank == a.fail_rank and a.fail_at >= 0:   # the first (graph) solve only
             gc.set_tuning("onepass_fail_at", a.fail_at)
         # every rank's set-up is finished before any rank's solve starts (nothing else on the GPU)
         torch.cuda.synchronize()

@@ -10,8 +10,9 @@ tests/golden/longrun_*.npz).  Here the same instance is rebuilt in HBM, proved i
 4096 sample points, b by SHA-256), solved on the device through the product path, and compared.
 
 Bound: north_star's 1e-5 relative l2 on x (the fixture stores the oracle's x in fp32, 6e-8
-relative); the error criterion trace within 1e-4 relative of the oracle's where it is above
-1e-6 of its first value (later values carry the trajectory's rounding sensitivity).
+relative; measured 1.6e-6 at configs[1]); the error criterion trace within 1e-4 relative or 1e-6
+of its first value absolute (its late values carry the trajectory's rounding sensitivity: measured
+within 7e-9 absolute at configs[1], where they are ~1e-7).
 """
 import hashlib
 import os
@@ -58,5 +59,4 @@ def test_long_horizon_against_oracle(name):
     print(f"{name} {m}x{n}, {IT} iterations: rel l2 vs oracle {e:.3e}")
     assert e <= 1e-5, e
     ref = fx["err_iter"][:IT]
-    big = ref > 1e-6 * ref[0]
-    np.testing.assert_allclose(res["err_iter"][:IT][big], ref[big], rtol=1e-4)
+    np.testing.assert_allclose(res["err_iter"][:IT], ref, rtol=1e-4, atol=1e-6 * ref[0])
