@@ -116,11 +116,16 @@ struct bpgl_ctx {
     // at 0.4 % of the iteration time
     int op_refresh = 256;
     int op_variant = 0;        // ring depth / prefetch variant (OpVar)
-    int op_cache = 0;          // permille of each row group read with cache-allocating loads
+    // permille of each row group read with cache-allocating loads (-1: auto, op_cache_auto)
+    int op_cache = -1;
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
     int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
     int op_rowb = 1;   // k_onepass_tail: residual update on blocks of its own ("tail_row_blocks" knob)
+    // fold the U partials inside k_onepass ("onepass_fold" 1) or in k_onepass_fold / the tail (0, default:
+    // the in-kernel form's write-through partials and segment barrier cost more than the launch it
+    // saves -- m = 1024 rows: k_onepass 55.0 -> 67.9 us against a 12.4 us fold; profiles/r03/fold_sweep)
+    int op_fold = 0;
     // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
     // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
     bool rows = false;
@@ -165,24 +170,37 @@ void geometry(bpgl_ctx* c) {
     c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
     c->op_gpl = SB > 64 ? 2 : 1;
     if (c->op_shape) {
-        int64_t ng = std::min<int64_t>(c->cus / SB, c->m);
+        int64_t ng = std::min<int64_t>(std::min<int64_t>(c->cus / SB, c->m), kOpMaxGroups);
         const int64_t R = cdiv(c->m, ng);
         ng = cdiv(c->m, R);
         c->op_SB = (int)SB;
         c->op_ngroups = (int)ng;
         c->op_R = (int)R;
         c->op_xl = (ng % 8 == 0) ? 1 : 0;   // each row group's blocks on one XCD (blockIdx % 8)
-        // k_onepass_tail: 64-column tiles and 256-row strides
-        c->op_tail_grid = (int)std::min<int64_t>(std::max(cdiv(c->m, kThreads), cdiv(c->wp, 64)), kOpTailBlocks);
+        // k_onepass_tail: 64-column tiles (one rank: one per block, its 4 waves split the row-group
+        // partials of U; row shards: U arrives summed, one tile per wave) and 256-row strides
+        c->op_tail_grid = c->rows ? (int)std::min<int64_t>(cdiv(c->wp, 64 * kWaves), kOpTailBlocks)
+                                  : (int)std::min<int64_t>(std::max(cdiv(c->m, kThreads), cdiv(c->wp, 64)), kOpTailBlocks);
     } else {
         c->op_SB = c->op_ngroups = c->op_R = c->op_xl = c->op_tail_grid = 0;
     }
 }
 
+// "onepass_cache_permille" = -1 (default): 750 when this rank's A block fits the 256 MiB Infinity
+// Cache give or take a quarter (the N = 8 row shard of the 8192 x 65536 matrix: k_onepass 57.5 ->
+// 52.2 us), else 0 (all non-temporal: at 512 MiB and 2 GiB cache-allocating loads cost 1-10 %).
+// Launches alternate the row direction, so the rows a launch read last are the next launch's first.
+// profiles/r03/strong_cache, profiles/r03/fold_sweep
+int op_cache_eff(const bpgl_ctx* c) {
+    if (c->op_cache >= 0) return c->op_cache;
+    const int64_t bytes = c->m * c->wp * (c->dtype == BPGL_F32 ? 4 : c->dtype == BPGL_F64 ? 8 : 2);
+    return bytes <= (int64_t)320 << 20 ? 750 : 0;
+}
+
 // scratch layout (offsets in bytes)
 struct Layout {
     int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opUs, opPG, opS, opABE,
-        total;
+        opSeg, opUsum, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -208,6 +226,8 @@ Layout layout(const bpgl_ctx* c) {
     L.opPG = k.take(op ? 8 * c->m * c->op_SB : 0);
     L.opS = k.take(op && c->rows ? 8 * c->m : 0);
     L.opABE = k.take(op && c->rows ? 8 * 4 : 0);
+    L.opSeg = k.take(op ? 8 * (int64_t)c->op_SB : 0);
+    L.opUsum = k.take(op && !c->rows ? 8 * c->wp : 0);
     L.total = k.off;
     return L;
 }
@@ -395,8 +415,18 @@ OnePassArgs op_tail_args(const bpgl_ctx* c) {
         o.Us = c->p.comm;
         o.ngroups = 1;
         if (xch_f32(c)) o.Uf = reinterpret_cast<const float*>(c->p.comm);
+    } else if (c->op.fold) {   // one rank: k_onepass folded U already
+        o.Us = c->op.Ufold;
+        o.ngroups = 1;
     }
     return o;
+}
+// the per-solve part of the one-pass arguments (after op_on is known): the in-kernel fold
+void op_configure(bpgl_ctx* c) {
+    if (!c->op_shape) return;
+    c->op.fold = c->op_on && c->op_fold ? 1 : 0;
+    c->op.rows_out = c->rows && c->op.fold ? 1 : 0;
+    c->op.Ufold32 = c->op.fold && xch_f32(c) ? reinterpret_cast<float*>(c->p.comm) : nullptr;
 }
 template <bool UPDATE>
 int onepass_tail(bpgl_ctx* c) {
@@ -534,12 +564,14 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
         ev_record(c, it, 7, 0);
         if ((rc = onepass_launch(c))) return rc;
         ev_record(c, it, 7, 1);
-        ev_record(c, it, 3, 0);
         float* xf = xch_f32(c) ? reinterpret_cast<float*>(c->p.comm) : nullptr;
-        hipLaunchKernelGGL(k_onepass_fold, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024)),
-                           dim3(kThreads), 0, c->stream, op_params(c), c->op, c->p.comm, xf);
-        LAUNCH_CHECK("k_onepass_fold");
-        ev_record(c, it, 3, 1);
+        if (!c->op.fold) {   // in-kernel fold: k_onepass wrote the exchange buffer itself
+            ev_record(c, it, 3, 0);
+            hipLaunchKernelGGL(k_onepass_fold, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024) + 1),
+                               dim3(kThreads), 0, c->stream, op_params(c), c->op, c->p.comm, xf);
+            LAUNCH_CHECK("k_onepass_fold");
+            ev_record(c, it, 3, 1);
+        }
         if (c->comm) {
             ev_record(c, it, 4, 0);
             if (xf) {
@@ -751,6 +783,7 @@ int recover_onepass(bpgl_ctx* c, DevState& st) {
             return fail(BPGL_E_EXCHANGE, "hand-off failure flag set outside the one-pass iteration at t = %lld",
                         (long long)t);
         c->op_on = false;
+        op_configure(c);
         c->n_fallback++;
         if ((rc = capture_graphs(c))) return rc;
         if (!st.done && c->req_t > t && (rc = step_impl(c, c->req_t - t))) return rc;
@@ -931,11 +964,16 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
         c->op.xl = c->op_xl;
         c->op.ls = c->rows ? 0 : 1;   // row shards: the line search follows the all-reduce (in the tail)
         c->op.abe = c->rows ? (double*)(s + L.opABE) : nullptr;
-        c->op.cache_permille = c->op_cache;
+        c->op.cache_permille = op_cache_eff(c);
+        c->op.segcnt = (unsigned long long*)(s + L.opSeg);
+        c->op.Ufold = c->rows ? p.comm : (double*)(s + L.opUsum);
     }
     c->op.fail_at = c->op_fail_at;
     HIP_TRY(hipSetDevice(c->device));
-    if (c->op_shape) HIP_TRY(hipMemsetAsync(s + L.opPG, 0, 8 * c->m * c->op_SB, c->stream));   // tag 0: never written
+    if (c->op_shape) {
+        HIP_TRY(hipMemsetAsync(s + L.opPG, 0, 8 * c->m * c->op_SB, c->stream));   // tag 0: never written
+        HIP_TRY(hipMemsetAsync(s + L.opSeg, 0, 8 * (int64_t)c->op_SB, c->stream));
+    }
     HIP_TRY(hipMemsetAsync(s + L.st, 0, sizeof(DevState), c->stream));
     HIP_TRY(hipMemsetAsync(s + L.D, 0, 8 * c->wp, c->stream));
     HIP_TRY(hipMemsetAsync(s + L.Dbuf, 0, 16 * c->wp, c->stream));
@@ -997,6 +1035,7 @@ int bpgl_set_shard(bpgl_ctx* c, int mode) {
     if (c->bound) return fail(BPGL_E_STATE, "bpgl_set_shard must precede bpgl_bind");
     if (mode == BPGL_SHARD_ROWS && c->nblock != 1) return fail(BPGL_E_ARG, "row shards need one feature block");
     c->rows = mode == BPGL_SHARD_ROWS;
+    geometry(c);   // the tail's grid differs for row shards
     return 0;
 }
 
@@ -1144,6 +1183,7 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
         if (c->rows && why && (c->external || !c->op_shape))
             return fail(BPGL_E_ARG, "external row shards run the one-pass iteration only: %s", why);
         c->op_on = c->onepass != 0 && !why;
+        op_configure(c);
         c->op_t = 0;
         c->op_refresh_pending = false;
         // external row shards: the caller runs the first exact gradient (phases 2 and 3)
@@ -1260,6 +1300,13 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->solver = false;
         return 0;
     }
+    if (!strcmp(key, "onepass_fold")) {   // speed only: where the U partials are summed (bitwise neutral for rows)
+        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "onepass_fold must be 0 or 1");
+        c->op_fold = (int)value;
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
     if (!strcmp(key, "tail_row_blocks")) {   // speed only: where the tail's residual update runs (bitwise neutral)
         if (value != 0 && value != 1) return fail(BPGL_E_ARG, "tail_row_blocks must be 0 or 1");
         c->op_rowb = (int)value;
@@ -1267,9 +1314,9 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         return 0;
     }
     if (!strcmp(key, "onepass_cache_permille")) {
-        if (value < 0 || value > 1000) return fail(BPGL_E_ARG, "onepass_cache_permille must be in [0, 1000]");
+        if (value < -1 || value > 1000) return fail(BPGL_E_ARG, "onepass_cache_permille must be -1 (auto) or in [0, 1000]");
         c->op_cache = (int)value;
-        c->op.cache_permille = c->op_cache;
+        c->op.cache_permille = op_cache_eff(c);
         drop_graphs(c);
         c->solver = false;
         return 0;

@@ -559,7 +559,21 @@ __device__ __forceinline__ double bld1_sc1(__amdgpu_buffer_rsrc_t r, long long o
 __device__ void fold_parts(const Params& p, int count, double& a, double& b, double& e) {
     __shared__ double sred[3][kWaves];
     a = 0.0; b = 0.0; e = 0.0;
-    for (int k = threadIdx.x; k < count; k += kThreads) {
+    int k = threadIdx.x;
+    for (; k + 3 * kThreads < count; k += 4 * kThreads) {   // 4 partials' loads in flight, adds in order
+        double v[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) v[u][c] = p.parts[4ll * (k + u * kThreads) + c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a += v[u][0];
+            b += v[u][1];
+            e = (v[u][2] > e || v[u][2] != v[u][2]) ? v[u][2] : e;
+        }
+    }
+    for (; k < count; k += kThreads) {
         a += p.parts[4ll * k];
         b += p.parts[4ll * k + 1];
         const double ek = p.parts[4ll * k + 2];

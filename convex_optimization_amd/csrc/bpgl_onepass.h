@@ -53,6 +53,7 @@ constexpr int kOpDelta = 1;     // rows between a row's phase 1 and its publicat
 constexpr int kOpMaxSB = 128;   // at most two granules per lane (GPL)
 constexpr unsigned kOpPolls = 1u << 16;
 constexpr int kOpTailBlocks = 1024;   // k_onepass_tail grid cap (= its shrink partial count)
+constexpr int kOpMaxGroups = 256;     // row groups (one block per CU: at most the CU count)
 
 struct OnePassArgs {
     double* G;                   // [wp]   gradient carried across iterations
@@ -67,6 +68,13 @@ struct OnePassArgs {
     long long fail_at;           // test hook: iteration whose launch reports a hand-off failure (-1: none)
     int rowb;                    // k_onepass_tail: blocks appended after the column blocks that only run
                                  // the residual update (0: the column blocks run it first, as before)
+    // in-kernel fold of the U partials ("onepass_fold" = 1): the ngroups blocks of a column segment
+    // meet at segcnt[sb] and each sums one slice of the segment's columns over the row groups
+    int fold;                    // 1: fold inside k_onepass (no k_onepass_fold launch)
+    unsigned long long* segcnt;  // [SB] arrivals per column segment (monotone, + ngroups per launch)
+    double* Ufold;               // [wp] the folded U (one rank: read by the tail; rows: the exchange buffer)
+    float* Ufold32;              // rows, fp32 exchange: the folded U as fp32 (instead of Ufold)
+    int rows_out;                // rows: the last block to arrive writes [r.s23 | s23.s23 | failed] and abe
 };
 
 typedef unsigned long long op_u64;
@@ -169,6 +177,85 @@ __device__ void op_linesearch(const Params& p, int ngroups) {
     if (threadIdx.x == 0 && !op_failed(p)) finish_step(p, rs, ss, a, b, e);
 }
 
+// Row shards, in-kernel fold: the last block of the launch to arrive writes the exchange tail
+// [r.s23 | s23.s23 | failed] (fixed-order sums over the row groups, as k_onepass_fold) and the
+// last shrink's folded partials (abe) for the line search at the head of k_onepass_tail.
+__device__ __forceinline__ void op_split_f32(double v, float* dst) {
+    const float hi = (float)v;
+    dst[0] = hi;
+    dst[1] = (float)(v - (double)hi);
+}
+__device__ void op_rows_scalars(const Params& p, const OnePassArgs& o) {
+    double a, b, e;
+    fold_parts(p, p.nparts, a, b, e);
+    if (threadIdx.x == 0) {
+        double rs = 0.0, ss = 0.0;
+        for (int q = 0; q < o.ngroups; ++q) { rs += ld_sc1(p.parts2 + 2ll * q); ss += ld_sc1(p.parts2 + 2ll * q + 1); }
+        const bool failed = op_failed(p);
+        if (o.Ufold32) {
+            op_split_f32(rs, o.Ufold32 + p.wp);
+            op_split_f32(ss, o.Ufold32 + p.wp + 2);
+            o.Ufold32[p.wp + 4] = failed ? 1.0f : 0.0f;
+        } else {
+            o.Ufold[p.wp] = rs;
+            o.Ufold[p.wp + 1] = ss;
+            o.Ufold[p.wp + 2] = failed ? 1.0 : 0.0;
+        }
+        o.abe[0] = a;
+        o.abe[1] = b;
+        o.abe[2] = e;
+    }
+}
+
+// In-kernel fold of the U partials (o.fold): every block has written its row group's partial of
+// its column segment through to memory (sc1); the ngroups blocks of segment sb meet at
+// segcnt[sb] (monotone: + ngroups per launch, so the launch's target is the next multiple of
+// ngroups), then block grp sums slice grp of the segment's BC columns over the groups in the
+// fixed order q = 0, 1, ... (the order of k_onepass_fold: the same bits) into Ufold / Ufold32.
+// The wait is bounded like the row hand-off: on exhaustion the launch reports a failure (its
+// blocks were not all resident) and commits nothing.  Returns false on that failure.
+template <int BC>
+__device__ bool op_fold_segment(const Params& p, const OnePassArgs& o, int grp, int sb) {
+    __shared__ int seg_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's partial is in memory
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long* c = o.segcnt + sb;
+        const unsigned long long ng = (unsigned long long)o.ngroups;
+        const unsigned long long old = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long target = (old / ng + 1) * ng;
+        unsigned n = kOpPolls;
+        int ok = 1;
+        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (n-- == 0) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        seg_ok = ok;
+    }
+    __syncthreads();
+    if (!seg_ok) return false;   // block-uniform
+    const int per = (BC + o.ngroups - 1) / o.ngroups;
+    const long long cend = (long long)sb * BC + BC < p.wp ? (long long)sb * BC + BC : p.wp;
+    const __amdgpu_buffer_rsrc_t ru = rsrc(o.Us, 8ll * o.ngroups * p.wp);
+    for (int j = threadIdx.x; j < per; j += kThreads) {
+        const long long c = (long long)sb * BC + (long long)grp * per + j;
+        if (c >= cend) break;
+        double acc = 0.0;
+        int q = 0;
+        for (; q + 8 <= o.ngroups; q += 8) {   // 8 loads in flight, then the adds in group order
+            double v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = bld1_sc1(ru, 8ll * ((long long)(q + k) * p.wp + c));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc += v[k];
+        }
+        for (; q < o.ngroups; ++q) acc += bld1_sc1(ru, 8ll * ((long long)q * p.wp + c));
+        if (o.Ufold32) o.Ufold32[c] = (float)acc;
+        else o.Ufold[c] = acc;
+    }
+    return true;
+}
+
 template <int LU, typename T>
 struct OnePassGeo {
     static constexpr int N = VecT<T>::N;
@@ -203,7 +290,17 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
     if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
         if (sb == 0 && threadIdx.x == 0) { st_sc1(p.parts2 + 2ll * grp, 0.0); st_sc1(p.parts2 + 2ll * grp + 1, 0.0); }
-        if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) op_linesearch(p, o.ngroups);
+        if (o.fold) {
+            const __amdgpu_buffer_rsrc_t ru = rsrc(o.Us + (long long)grp * p.wp, 8ll * p.wp);
+            for (int j = threadIdx.x; j < G::BC; j += kThreads)
+                if ((long long)sb * G::BC + j < p.wp) bst1_sc1(ru, 8ll * ((long long)sb * G::BC + j), 0.0);
+            if (!op_fold_segment<G::BC>(p, o, grp, sb) && threadIdx.x == 0)
+                atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
+        }
+        if ((o.ls || o.rows_out) && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) {
+            if (o.ls) op_linesearch(p, o.ngroups);
+            else op_rows_scalars(p, o);
+        }
         return;
     }
     const unsigned tag = (unsigned)((p.st->op_epoch + 1) & 1);   // bound scratch is zero: parity 0 = unwritten
@@ -368,13 +465,27 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         if (lane == 0) { st_sc1(p.parts2 + 2ll * grp, rs); st_sc1(p.parts2 + 2ll * grp + 1, ss); }
     }
     double* dst = o.Us + (long long)grp * p.wp;
+    if (o.fold) {   // block-uniform
+        // written through (sc1): the blocks of this segment in the other row groups (other XCDs) read it
+        const __amdgpu_buffer_rsrc_t ru = rsrc(dst, 8ll * p.wp);
 #pragma unroll
-    for (int k = 0; k < LU; ++k)
-        if (colok[k])
+        for (int k = 0; k < LU; ++k)
+            if (colok[k])
 #pragma unroll
-            for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
-    if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x))   // block-uniform
-        op_linesearch(p, o.ngroups);
+                for (int e = 0; e < N; e += 2) bst2_sc1(ru, 8ll * (col[k] + e), u[k][e], u[k][e + 1]);
+        if (!op_fold_segment<G::BC>(p, o, grp, sb) && threadIdx.x == 0)
+            atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
+    } else {
+#pragma unroll
+        for (int k = 0; k < LU; ++k)
+            if (colok[k])
+#pragma unroll
+                for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
+    }
+    if ((o.ls || o.rows_out) && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) {   // block-uniform
+        if (o.ls) op_linesearch(p, o.ngroups);
+        else op_rows_scalars(p, o);
+    }
 }
 
 // Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23 |
@@ -386,31 +497,41 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
 // xGMI.  With one rank the pair carries the scalar to ~2^-48; RCCL sums the hi words and the
 // lo words separately in fp32, so with several ranks each summed word is rounded to fp32 and
 // the scalars are only fp32-accurate (~2^-24 relative).
-__device__ __forceinline__ void op_split_f32(double v, float* dst) {
-    const float hi = (float)v;
-    dst[0] = hi;
-    dst[1] = (float)(v - (double)hi);
-}
 __global__ __launch_bounds__(kThreads) void k_onepass_fold(Params p, OnePassArgs o, double* __restrict__ out,
                                                            float* __restrict__ outf) {
-    const long long stride = (long long)gridDim.x * kThreads;
-    for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < p.wp; j += stride) {
-        double acc = 0.0;
-        for (int q = 0; q < o.ngroups; ++q) acc += o.Us[(long long)q * p.wp + j];
-        if (outf) outf[j] = (float)acc;
-        else out[j] = acc;
+    const int cblocks = (int)gridDim.x - 1;   // the last block folds the scalars
+    if ((int)blockIdx.x < cblocks) {
+        const long long stride = (long long)cblocks * kThreads;
+        for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < p.wp; j += stride) {
+            // 8 loads in flight, then the adds in group order (the same bits as one at a time)
+            double acc = 0.0;
+            int q = 0;
+            for (; q + 8 <= o.ngroups; q += 8) {
+                double v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = o.Us[(long long)(q + k) * p.wp + j];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc += v[k];
+            }
+            for (; q < o.ngroups; ++q) acc += o.Us[(long long)q * p.wp + j];
+            if (outf) outf[j] = (float)acc;
+            else out[j] = acc;
+        }
+        return;
     }
-    // block 0 also folds the last shrink's per-block partials (identical on every rank: x, g and
-    // D are replicated) for the line search at the head of k_onepass_tail -- the fold k_linesearch
-    // ran, in the same order (p.nparts = the tail's grid)
-    if (o.abe && blockIdx.x == 0) {   // block-uniform
-        double a, b, e;
-        fold_parts(p, p.nparts, a, b, e);
-        if (threadIdx.x == 0) { o.abe[0] = a; o.abe[1] = b; o.abe[2] = e; }
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the last shrink's per-block partials (identical on every rank: x, g and D are replicated) for
+    // the line search at the head of k_onepass_tail -- the fold k_linesearch ran, in the same order
+    // (p.nparts = the tail's grid); the groups' [r.s23, s23.s23] staged through LDS by all lanes at
+    // once, then summed by one thread in group order
+    __shared__ double pr[2 * kOpMaxGroups];
+    for (int k = threadIdx.x; k < 2 * o.ngroups; k += kThreads) pr[k] = p.parts2[k];
+    double a = 0.0, b = 0.0, e = 0.0;
+    if (o.abe) fold_parts(p, p.nparts, a, b, e);   // has a barrier
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (o.abe) { o.abe[0] = a; o.abe[1] = b; o.abe[2] = e; }
         double rs = 0.0, ss = 0.0;
-        for (int q = 0; q < o.ngroups; ++q) { rs += p.parts2[2ll * q]; ss += p.parts2[2ll * q + 1]; }
+        for (int q = 0; q < o.ngroups; ++q) { rs += pr[2 * q]; ss += pr[2 * q + 1]; }
         const bool failed = op_failed(p);
         if (outf) {
             op_split_f32(rs, outf + p.wp);
@@ -471,21 +592,59 @@ __global__ __launch_bounds__(kThreads) void k_recip(const double* __restrict__ d
 // (it runs in the iteration whose line search stops, too).
 template <bool UPDATE>
 __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs o) {
+    // Every load the head needs is issued before the first decision (one memory round trip
+    // instead of four dependent ones): the state words, the exchange scalars and the fold's sums
+    // (row shards), and the operands of this wave's first column tile (pre-summed U).
+    const bool b0 = blockIdx.x == 0 && threadIdx.x == 0;
+    const long long done = p.st->done;
+    const bool opf = UPDATE && op_failed(p);
+    const unsigned long long ran = (UPDATE && b0) ? p.st->op_ran : 0ull;
+    const long long epoch = (UPDATE && b0) ? p.st->op_epoch : 0;
+    double gamma = UPDATE ? p.st->gamma : 0.0;
+    double xfail = 0.0, rs = 0.0, ss = 0.0, a = 0.0, b = 0.0, e = 0.0;
+    if (UPDATE && o.abe) {   // row shards
+        if (o.Uf) {
+            xfail = (double)o.Uf[p.wp + 4];
+            rs = (double)o.Uf[p.wp] + (double)o.Uf[p.wp + 1];
+            ss = (double)o.Uf[p.wp + 2] + (double)o.Uf[p.wp + 3];
+        } else {
+            xfail = o.Us[p.wp + 2];
+            rs = o.Us[p.wp];
+            ss = o.Us[p.wp + 1];
+        }
+        a = o.abe[0];
+        b = o.abe[1];
+        e = o.abe[2];
+    }
+    const int cb0 = (int)gridDim.x - (UPDATE ? o.rowb : 0);   // column blocks
+    const int lane0 = threadIdx.x & 63, wave0 = threadIdx.x >> 6;
+    // pre-summed U (row shards, or one rank after the in-kernel fold): each wave owns 64-column tiles
+    const long long tile0 = (long long)blockIdx.x * kWaves + wave0;
+    const long long j0 = tile0 * 64 + lane0;
+    const bool pre = o.ngroups == 1 && (int)blockIdx.x < cb0 && j0 < p.wp;
+    double pg = 0.0, pu = 0.0, px = 0.0, pd = 0.0, pdg = 0.0, prc = 0.0;
+    if (pre) {
+        const bool col = j0 < p.w;
+        pg = o.G[j0];
+        pu = !UPDATE ? 0.0 : o.Uf ? (double)o.Uf[j0] : o.Us[j0];
+        px = col ? p.x[j0] : 0.0;
+        pd = (UPDATE && col) ? p.D[j0] : 0.0;
+        pdg = col ? p.diag[j0] : 0.0;
+        prc = col ? p.rec[j0] : 0.0;
+    }
     // the parity advances after every k_onepass launch, a failed one too (it still published
     // every granule of its rows)
-    if (UPDATE && blockIdx.x == 0 && threadIdx.x == 0 && p.st->op_ran) {
-        p.st->op_epoch += 1;
+    if (UPDATE && b0 && ran) {
+        p.st->op_epoch = epoch + 1;
         p.st->op_ran = 0;
     }
-    if (p.st->done) return;
+    if (done) return;
     // a failed k_onepass (this iteration or an earlier one not yet re-run) commits nothing
-    if (UPDATE && op_failed(p)) return;
-    double gamma = UPDATE ? p.st->gamma : 0.0;
+    if (UPDATE && opf) return;
     if (UPDATE && o.abe) {
         // row shards: any rank's failure, summed over ranks -> every rank skips this iteration
-        const double failed = o.Uf ? (double)o.Uf[p.wp + 4] : o.Us[p.wp + 2];
-        if (failed != 0.0) {   // grid-uniform
-            if (blockIdx.x == 0 && threadIdx.x == 0)
+        if (xfail != 0.0) {   // grid-uniform
+            if (b0)
                 __hip_atomic_store(reinterpret_cast<unsigned long long*>(&p.st->op_fail), 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             return;
@@ -497,15 +656,6 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
         // arithmetic as k_linesearch: rs and ss are the sums of one value each).  One feature
         // block: the stop rule is err < err_bound in this iteration (block_cnt never carries).
         // Block 0 records the state (finish_step); a block that finds the rule fired updates nothing.
-        double rs, ss;
-        if (o.Uf) {
-            rs = (double)o.Uf[p.wp] + (double)o.Uf[p.wp + 1];
-            ss = (double)o.Uf[p.wp + 2] + (double)o.Uf[p.wp + 3];
-        } else {
-            rs = o.Us[p.wp];
-            ss = o.Us[p.wp + 1];
-        }
-        const double a = o.abe[0], b = o.abe[1], e = o.abe[2];
         const double r1 = rs + p.mu * (a - b);
         gamma = (ss == 0.0) ? 0.0 : proj(-r1 / ss, 0.0, 1.0);
         const bool stop = p.err_bound >= 0.0 && e < p.err_bound;
@@ -557,9 +707,10 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
         p.D[j] = Dj;
     };
     if (o.ngroups == 1) {
-        // row shards (U already summed over ranks): every wave takes its own 64-column tiles
-        for (long long tile = (long long)blockIdx.x * kWaves + wave; tile < ntile;
-             tile += (long long)cb * kWaves) {
+        // U already summed (over ranks, or by k_onepass): every wave takes its own 64-column tiles;
+        // the first tile's operands were loaded at the head
+        if (pre) shrink_col(j0, pg, pu, px, pd, pdg, prc);
+        for (long long tile = tile0 + (long long)cb * kWaves; tile < ntile; tile += (long long)cb * kWaves) {
             const long long j = tile * 64 + lane;
             if (j >= p.wp) continue;
             const bool col = j < p.w;

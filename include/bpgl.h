@@ -255,9 +255,13 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   one feature block, one rank (or row shards), no fused mode, at most
  *   128 x 4096 columns (fp32; 128 x 6144 for bf16, 128 x 2048 for fp64) and all
  *   of its blocks resident at once (nothing else running on the device).
- *   "onepass_cache_permille" (default 0): share of every row group the one-pass
- *   kernel reads with cache-allocating loads (launches alternate the row
- *   direction, so the next launch starts on those rows).
+ *   "onepass_cache_permille" (default -1 = auto: 750 when this rank's A block is
+ *   at most 320 MiB, i.e. about the 256 MiB Infinity Cache, else 0): share of every
+ *   row group the one-pass kernel reads with cache-allocating loads (launches
+ *   alternate the row direction, so the next launch starts on those rows).
+ *   "onepass_fold" (default 0): 1 sums the row groups' U partials inside k_onepass
+ *   (write-through partials + a per-segment barrier) instead of in k_onepass_fold
+ *   (row shards) / k_onepass_tail (one rank) -- measured slower, kept as an option.
  *   "onepass_variant" (default 0, 0-3): register-ring depth / prefetch distance.
  *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
