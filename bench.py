@@ -464,16 +464,22 @@ def cpu_baseline(gc, b, mu, seconds, cores, cpu_info, share_note=""):
         return n / (time.perf_counter() - t0), n
     A64 = A.astype(np.float64)
     dg = np.square(A64).sum(axis=0)
-    v, n_np = numpy_rate(A64, seconds / 3)
-    out["numpy_fp64"] = {"value": v, "unit": "iters/s",
+    # three samples (the rate moves 12-40 it/s between boxes and runs on a shared host): the
+    # median is the value, the three are reported as its range
+    runs = [numpy_rate(A64, seconds / 9) for _ in range(3)]
+    rates = sorted(r[0] for r in runs)
+    v, n_np = rates[1], runs[0][1]
+    out["numpy_fp64"] = {"value": v, "unit": "iters/s", "samples": [r[0] for r in runs],
+                         "range": [rates[0], rates[2]],
                          "threads": "OpenBLAS default (OMP_NUM_THREADS=" + os.environ.get("OMP_NUM_THREADS", "unset") + ")",
-                         "sample": f"oracle.run_numpy, {n_np} iterations from x=0 on the same A (as fp64), set-up excluded"}
+                         "sample": f"oracle.run_numpy, median of 3 samples of {n_np} iterations from x=0 on the same A "
+                                   "(as fp64), set-up excluded"}
     # the reported baseline: the reference's own CPU arithmetic (cpu_calculation.py's numpy GEMVs at
     # its default TYPE double, lasso.py:102-157) restated, on this job's cores -- the fastest of the
     # fp64 CPU paths timed here; the C oracle and the fp32-storage variant stay beside it
-    out.update({"value": v, "unit": "iters/s", "cores": threads, "kind": "port",
-                "sample": f"oracle.run_numpy (the reference iteration in numpy, fp64 OpenBLAS GEMVs), {n_np} "
-                          f"iterations from x=0 on the same {H}x{gc.Block * W} A and b{share_note}, "
+    out.update({"value": v, "unit": "iters/s", "cores": threads, "kind": "port", "range": [rates[0], rates[2]],
+                "sample": f"oracle.run_numpy (the reference iteration in numpy, fp64 OpenBLAS GEMVs), median of 3 "
+                          f"samples of {n_np} iterations from x=0 on the same {H}x{gc.Block * W} A and b{share_note}, "
                           f"set-up (diag) excluded, OpenBLAS on {threads} threads"})
     # and the fp32-storage variant (the reference's TYPE='float' CPU path: sgemv on fp32 A, fp64 elsewhere)
     del A64
@@ -554,6 +560,22 @@ def pmc_traffic(workload_key, kernel):
 
 
 MFMA_BF16_DENSE_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def mfma_counters(kernel, k):
+    """MFMA utilisation of a panel pass from rocprofv3 counters (profiles/mfma_util.json, written by
+    tools/mfma_util.py from tools/panel_mfma_pmc.sh): SQ_VALU_MFMA_BUSY_CYCLES over SIMDs x kernel
+    cycles (GRBM_GUI_ACTIVE / 8), at the clock the chip ran and at the 2.4 GHz peak clock, or None"""
+    try:
+        e = json.load(open(os.path.join(ROOT, "profiles", "mfma_util.json")))[f"{kernel}_k{k}"]
+    except Exception:
+        return None
+    return {"busy_cycles_per_launch": e["busy_cycles"], "mfma_instructions": e["mfma_instructions"],
+            "busy_frac_at_running_clock": e["busy_frac_at_running_clock"],
+            "busy_frac_at_peak_clock": e.get("busy_frac_at_peak_clock"),
+            "running_clock_hz_est": e.get("running_clock_hz_est"),
+            "source": "profiles/mfma_util.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_BF16, "
+                      "GRBM_GUI_ACTIVE; tools/panel_mfma_pmc.sh)"}
 
 
 LDS_FILL_CAP_GBS = 9600.0   # best LDS-DMA fill rate measured on a panel pass, summed over CUs (DESIGN.md section 3b)
@@ -678,7 +700,8 @@ def main_panel(args):
             "iteration_frac_end_to_end": alg_iter / (el_graph / args.steps) / (HBM_PEAK_GBS * 1e9),
             "survey_two_pass_frac": alg_iter / (el_graph / args.steps) / (HBM_PEAK_GBS * 1e9),
             "mfma": {"achieved_tflops": tflops, "peak_tflops": MFMA_BF16_DENSE_TFLOPS,
-                     "frac": tflops / MFMA_BF16_DENSE_TFLOPS, "flops_per_launch": flops},
+                     "frac": tflops / MFMA_BF16_DENSE_TFLOPS, "flops_per_launch": flops,
+                     "counters": mfma_counters({"pass1_mfma": "k_panel_pass1", "pass2_mfma": "k_panel_pass2"}[dom], k)},
             # the bound the k-sweep points at: every byte of A and of the k-wide
             # operand enters LDS through each CU's global_load_lds path; summed over the blocks of a
             # launch, against the best rate that path sustained in any panel pass (9.6 TB/s = 37.5 GB/s

@@ -149,3 +149,32 @@ def test_pool_baseline_matches_oracle():
     ref = oracle.run(A, bb, mu, 2, 12, P=4)["x"]
     assert np.linalg.norm(x - ref) <= 1e-10 * np.linalg.norm(ref)
     assert largest_divisor_at_most(2048, 12) == 8 and largest_divisor_at_most(2048, 64) == 64
+
+
+def test_multi_gpu_legs_carry_both_splits():
+    """the N > 1 line's side legs (bench.leg_summary): value in the leg's unit, per-rank all-reduce
+    times, and the iteration form; window_rate takes the median of the valid windows only"""
+    b = _bench()
+
+    class FakeGC:
+        shard = "columns"
+
+    wins = [{"s": 0.1, "s_amortised": 0.1, "valid": True}, {"s": 0.5, "s_amortised": 0.5, "valid": False},
+            {"s": 0.2, "s_amortised": 0.2, "valid": True}, {"s": 0.3, "s_amortised": 0.3, "valid": True}]
+    res = {"windows": wins, "kernel_ms": {"colpass": 0.3, "rowpass": 0.3, "allreduce": 0.02, "onepass": 0.0},
+           "m_local": 8192, "w_local": 65536, "gc": FakeGC(), "fallbacks": 0, "cus": 256}
+    v, raw = b.window_rate(res, 100)
+    assert abs(v - 100 / 0.2) < 1e-9 and abs(raw - 0.2 / 100) < 1e-12
+
+    class TwoRanks(b.SoloCtx):
+        def gather(self, x):
+            return [float(x), float(x) + 1e-3]
+
+    ctx = TwoRanks(type("C", (), {"local": 0})())
+    weak = b.leg_summary(ctx, res, 100, 2, True)
+    assert weak["value"] == 2 * v and weak["unit"] == "block-iters/s" and weak["split"] == "columns"
+    assert weak["iteration"] == "two passes over A" and len(weak["allreduce_ms_per_rank"]) == 2
+    strong = b.leg_summary(ctx, res, 100, 2, False)
+    assert strong["value"] == v and strong["unit"] == "iters/s"
+    solo = b.SoloCtx(type("C", (), {"local": 3})())
+    assert (solo.rank, solo.world, solo.local) == (0, 1, 3) and solo.max(2.0) == 2.0 and solo.gather(1) == [1.0]

@@ -224,8 +224,9 @@ def test_panel_deferred_x_update_agrees(d_split):
 
 def test_panel_full_configs4_shape_matches_oracle():
     """BASELINE configs[4] at full size (m = 8192, n = 65536, k = 128, bf16 A): two RHS against the
-    fp64 oracle after 30 iterations, at the stated tolerance (x 1e-2, objective 1e-5; measured at
-    100 iterations: x 1.8e-6, objective 5e-10 -- profiles/r01/sweeps/panel_dsplit_accuracy.json)."""
+    fp64 oracle after 30 iterations: x within 1e-3 relative l2 (tightened from SURVEY's 1e-2; measured
+    at 100 iterations 1.8e-6, at 400 iterations 2.6-6.7e-5 -- profiles/r01/sweeps/panel_dsplit_accuracy.json,
+    profiles/r02/longrun/configs4_400.json), objective within 1e-5."""
     m, n, k, it = 8192, 65536, 128, 30
     g = torch.Generator(device="cuda").manual_seed(5)
     A = torch.randn(m, n, device="cuda", generator=g)
@@ -242,6 +243,8 @@ def test_panel_full_configs4_shape_matches_oracle():
     del A64
     for j in (0, 127):
         ref = oracle.run(Ah, Bh[:, j], float(mu[j]), 1, it, nthreads=NT)["x"]
-        assert np.linalg.norm(X[:, j] - ref) <= 1e-2 * np.linalg.norm(ref)
+        ex = np.linalg.norm(X[:, j] - ref) / np.linalg.norm(ref)
+        print(f"configs[4] RHS {j}, {it} iterations: x rel l2 vs oracle {ex:.3e}")
+        assert ex <= 1e-3, ex
         f_dev, f_ref = objective(Ah, Bh[:, j], mu[j], X[:, j]), objective(Ah, Bh[:, j], mu[j], ref)
         assert abs(f_dev - f_ref) <= 1e-5 * f_ref, (j, abs(f_dev - f_ref) / f_ref)
