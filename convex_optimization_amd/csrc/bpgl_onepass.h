@@ -709,16 +709,28 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
     if (o.ngroups == 1) {
         // U already summed (over ranks, or by k_onepass): every wave takes its own 64-column tiles;
         // the first tile's operands were loaded at the head
-        if (pre) shrink_col(j0, pg, pu, px, pd, pdg, prc);
-        for (long long tile = tile0 + (long long)cb * kWaves; tile < ntile; tile += (long long)cb * kWaves) {
-            const long long j = tile * 64 + lane;
-            if (j >= p.wp) continue;
-            const bool col = j < p.w;
-            const double g = o.G[j];
-            const double u = !UPDATE ? 0.0 : o.Uf ? (double)o.Uf[j] : o.Us[j];
-            const double xj = col ? p.x[j] : 0.0, dold = (UPDATE && col) ? p.D[j] : 0.0;
-            const double dg = col ? p.diag[j] : 0.0, rc = col ? p.rec[j] : 0.0;
-            shrink_col(j, g, u, xj, dold, dg, rc);
+        // (software-pipelined: the next tile's operands are loaded before this tile's shrink stores,
+        // which the compiler could not move them past -- D and x are written in place)
+        const long long tstep = (long long)cb * kWaves;
+        bool have = pre;
+        long long j = j0;
+        for (long long tile = tile0; tile < ntile; tile += tstep) {   // wave-uniform bounds
+            const long long jn = j + tstep * 64;
+            const bool hn = tile + tstep < ntile && jn < p.wp;
+            double ng = 0.0, nu = 0.0, nx = 0.0, nd = 0.0, ndg = 0.0, nrc = 0.0;
+            if (hn) {
+                const bool col = jn < p.w;
+                ng = o.G[jn];
+                nu = !UPDATE ? 0.0 : o.Uf ? (double)o.Uf[jn] : o.Us[jn];
+                nx = col ? p.x[jn] : 0.0;
+                nd = (UPDATE && col) ? p.D[jn] : 0.0;
+                ndg = col ? p.diag[jn] : 0.0;
+                nrc = col ? p.rec[jn] : 0.0;
+            }
+            if (have) shrink_col(j, pg, pu, px, pd, pdg, prc);
+            have = hn;
+            j = jn;
+            pg = ng; pu = nu; px = nx; pd = nd; pdg = ndg; prc = nrc;
         }
     } else
     // one rank: tiles of 64 (lane = column); the 4 waves split the row-group partials of U

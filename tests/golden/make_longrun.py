@@ -9,7 +9,7 @@ cpu_vs_gpu.py:66 -- from x = 0.  The fixture keeps x (fp32: 6e-8 relative, far i
 bound), err_iter, mu, a SHA-256 of b and A at 4096 sample points, so the GPU test
 (tests/test_longrun.py) can check it rebuilt the same instance before comparing.
 
-usage: python tests/golden/make_longrun.py [configs1 configs3 configs2] [--iters 1000] [--threads 8]
+usage: python tests/golden/make_longrun.py [configs1 configs3 configs2 configs4] [--iters 1000] [--threads 8]
 """
 import argparse
 import hashlib
@@ -27,16 +27,48 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import hash_instance as H  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-SHAPES = {"configs1": (8192, 65536), "configs3": (1048576, 4096), "configs2": (8192, 524288)}
+SHAPES = {"configs1": (8192, 65536), "configs3": (1048576, 4096), "configs2": (8192, 524288),
+          "configs4": (8192, 65536)}
+PANEL_K, PANEL_RHS = 128, (0, 127)   # configs[4]: k right-hand sides; the two the oracle follows
+
+
+def panel_case(a):
+    """configs[4]: bf16 A (exact hash values), k = 128 right-hand sides; the oracle runs the
+    single-RHS iteration on RHS 0 and 127 (the panel path solves each RHS with it, lasso.py:102-157)."""
+    m, n = SHAPES["configs4"]
+    t0 = time.time()
+    A = H.np_A_bf16(m, n)
+    out = dict(m=m, n=n, k=PANEL_K, iters=a.iters, rhs=np.array(PANEL_RHS), threads=a.threads)
+    rows, cols = H.sample_points(m, n)
+    out.update(A_rows=rows, A_cols=cols, A_samples=A[rows, cols])
+    for r in PANEL_RHS:
+        b = H.np_b_rhs(A, r)
+        mu = 0.1 * float(np.abs(oracle.mtv(A, 0, n, b, nthreads=a.threads)).max())
+        t1 = time.time()
+        ref = oracle.run(A, b, mu, 1, a.iters, nthreads=a.threads)
+        res = A.astype(np.float64) @ ref["x"] - b
+        out[f"mu_{r}"] = mu
+        out[f"x_{r}"] = ref["x"].astype(np.float32)
+        out[f"x_norm_{r}"] = np.linalg.norm(ref["x"])
+        out[f"objective_{r}"] = 0.5 * res @ res + mu * np.abs(ref["x"]).sum()
+        out[f"err_iter_{r}"] = ref["err_iter"]
+        out[f"b_sha256_{r}"] = hashlib.sha256(b.tobytes()).hexdigest()
+        print(f"configs4 RHS {r}: mu {mu:.17g}, {a.iters} oracle iterations in {time.time() - t1:.1f} s", flush=True)
+    path = os.path.join(HERE, "longrun_configs4.npz")
+    np.savez_compressed(path, **out)
+    print(f"configs4: {time.time() - t0:.1f} s -> {path}, {os.path.getsize(path)} B", flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="*", default=list(SHAPES))
+    ap.add_argument("which", nargs="*", default=list(SHAPES))   # configs4: the bf16 k-RHS panel case
     ap.add_argument("--iters", type=int, default=1000)
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     a = ap.parse_args()
     for name in a.which:
+        if name == "configs4":
+            panel_case(a)
+            continue
         m, n = SHAPES[name]
         t0 = time.time()
         A = H.np_A(m, n)

@@ -120,3 +120,78 @@ def sample_points(m, n, k=4096, seed=7):
     rows = np.concatenate([[0, m - 1], rs.randint(0, m, k - 2)])
     cols = np.concatenate([[0, n - 1], rs.randint(0, n, k - 2)])
     return rows.astype(np.int64), cols.astype(np.int64)
+
+
+# ---------------------------------------------------------------- configs[4]: bf16 A, k right-hand sides
+# A[i, j] = (h(i n + j, sA) >> 24 - 128) 2^-s, s = round(log2 sqrt(n * 5461)) (rows ~unit norm): an
+# integer of at most 8 significant bits times a power of two, exact in bf16.  X_true[:, r] and e[:, r] as
+# above with the seeds offset per right-hand side r; B = A X_true + E exact in fp64 in any summation
+# order (terms on the 2^-34 grid, partial sums below 2^12 at m = 8192, n = 65536).
+SEED_XK, SEED_EK = 0x4567891, 0x5678912
+
+
+def bf16_scale(n):
+    return 2.0 ** -round(math.log2(math.sqrt(n * 5461.0)))
+
+
+def np_A_bf16(m, n, chunk_rows=None):
+    """as float32 (every value exact in bf16)"""
+    chunk_rows = chunk_rows or max(1, (1 << 26) // n)
+    A = np.empty((m, n), dtype=np.float32)
+    sc = np.float32(bf16_scale(n))
+    for i0 in range(0, m, chunk_rows):
+        i1 = min(m, i0 + chunk_rows)
+        idx = np.arange(i0 * n, i1 * n, dtype=np.int64)
+        A[i0:i1] = (((_hash(idx, SEED_A, np) >> 24) - 128).astype(np.float32) * sc).reshape(i1 - i0, n)
+    return A
+
+
+def torch_A_bf16(m, n, device, chunk_rows=None):
+    import torch
+    chunk_rows = chunk_rows or max(1, (1 << 26) // n)
+    A = torch.empty((m, n), dtype=torch.float32, device=device)
+    sc = bf16_scale(n)
+    for i0 in range(0, m, chunk_rows):
+        i1 = min(m, i0 + chunk_rows)
+        idx = torch.arange(i0 * n, i1 * n, dtype=torch.int64, device=device)
+        A[i0:i1] = (((_hash(idx, SEED_A, torch) >> 24) - 128).to(torch.float32) * sc).reshape(i1 - i0, n)
+    return A
+
+
+def np_x_true_rhs(n, r):
+    h = _hash(np.arange(n, dtype=np.int64) + np.int64(r) * n, SEED_XK, np)
+    keep = (h & 0xFFFF) < int(0.4 * 65536)
+    c = ((h >> 16) % 6).astype(np.int64)
+    c = np.where(c < 3, c - 3, c - 2)
+    return np.where(keep, c, 0).astype(np.float64)
+
+
+def np_e_rhs(m, r):
+    u = (_hash(np.arange(m, dtype=np.int64) + np.int64(r) * m, SEED_EK, np) >> 8) - (1 << 23)
+    return u.astype(np.float64) * 2.0 ** -34
+
+
+def np_b_rhs(A, r, chunk_rows=None):
+    """column r of B (A as produced by np_A_bf16)"""
+    m, n = A.shape
+    x = np_x_true_rhs(n, r)
+    chunk_rows = chunk_rows or max(1, (1 << 25) // n)
+    b = np.empty(m)
+    for i0 in range(0, m, chunk_rows):
+        i1 = min(m, i0 + chunk_rows)
+        b[i0:i1] = A[i0:i1].astype(np.float64) @ x
+    return b + np_e_rhs(m, r)
+
+
+def torch_B(A, k):
+    """(m, k) fp64 right-hand sides for the torch A of torch_A_bf16"""
+    import torch
+    m, n = A.shape
+    dev = A.device
+    X = torch.from_numpy(np.stack([np_x_true_rhs(n, r) for r in range(k)], axis=1)).to(dev)
+    E = torch.from_numpy(np.stack([np_e_rhs(m, r) for r in range(k)], axis=1)).to(dev)
+    B = torch.empty((m, k), dtype=torch.float64, device=dev)
+    for i0 in range(0, m, 1024):
+        i1 = min(m, i0 + 1024)
+        B[i0:i1] = A[i0:i1].double() @ X
+    return B + E

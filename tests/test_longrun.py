@@ -60,3 +60,38 @@ def test_long_horizon_against_oracle(name):
     assert e <= 1e-5, e
     ref = fx["err_iter"][:IT]
     np.testing.assert_allclose(res["err_iter"][:IT], ref, rtol=1e-4, atol=1e-6 * ref[0])
+
+
+@pytest.mark.timeout(600)
+def test_panel_long_horizon_against_oracle():
+    """configs[4] (8192 x 65536 bf16 A, k = 128 right-hand sides), ITER_MAX = 1000 iterations of the
+    panel path (MFMA passes with hi + lo residual / direction), RHS 0 and 127 against the fp64 oracle on
+    the same bf16 A: x within 1e-3 relative l2 (the bound stated for this path, tests/test_panel.py), the
+    objective within 1e-5 relative."""
+    from convex_optimization_amd.panel import PanelLasso
+    path = os.path.join(GOLD, "longrun_configs4.npz")
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not generated (tests/golden/make_longrun.py configs4)")
+    fx = dict(np.load(path))
+    m, n, k, IT = int(fx["m"]), int(fx["n"]), int(fx["k"]), int(fx["iters"])
+    A = H.torch_A_bf16(m, n, "cuda:0")
+    rows, cols = torch.from_numpy(fx["A_rows"]).cuda(), torch.from_numpy(fx["A_cols"]).cuda()
+    assert np.array_equal(A[rows, cols].cpu().numpy(), fx["A_samples"]), "A differs from the fixture's"
+    B = H.torch_B(A, k)
+    A64 = A.double()
+    mu = (0.1 * (A64.t() @ B).abs().amax(dim=0)).cpu().numpy()
+    for r in fx["rhs"]:
+        assert hashlib.sha256(B[:, int(r)].cpu().numpy().tobytes()).hexdigest() == str(fx[f"b_sha256_{r}"])
+        mu[int(r)] = float(fx[f"mu_{r}"])
+    pl = PanelLasso(A, 1, nrhs=k, device=0)
+    X = pl.run(B, mu, IT)["x"]
+    for r in fx["rhs"]:
+        r = int(r)
+        ex = rel(X[:, r], fx[f"x_{r}"])
+        x = torch.from_numpy(X[:, r]).cuda()
+        res = A64 @ x - B[:, r]
+        f = 0.5 * float(res @ res) + float(mu[r]) * float(x.abs().sum())
+        ef = abs(f - float(fx[f"objective_{r}"])) / float(fx[f"objective_{r}"])
+        print(f"configs4 RHS {r}, {IT} iterations: x rel l2 vs oracle {ex:.3e}, objective rel {ef:.3e}")
+        assert ex <= 1e-3, ex
+        assert ef <= 1e-5, ef
