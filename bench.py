@@ -26,7 +26,8 @@ across column shards, it is the reference's two passes (A^T r, then A D).
           8192 x 65536 matrix split N ways by rows), "columns" (the reference's
           column split of the same weak problem, and its strong form), each with
           its per-rank all-reduce times, and "n1_same_run" (rank 0 alone on the
-          N = 1 problem, with the efficiencies of the legs against it).
+          N = 1 problem, with the efficiencies of the legs against it) and
+          "rows_exchange_fp32" (the row split with the opt-in fp32 exchange).
   --config 2: configs[2]'s own problem (m=8192 n=524288) split over the N GPUs
           (strong scaling; at N = 1 the whole 16 GiB matrix on one GPU).
   --config 3 / 4: configs[3] (1048576 x 4096 fp32) / configs[4] (k = 128
@@ -866,6 +867,17 @@ def main():
             res = measure(ctx, argparse.Namespace(**vars(args)), m, args.n_per_gpu)
             out["strong"] = leg_summary(ctx, res, K, G, False)
             out["strong"]["config"] = f"m={m} n={args.n_per_gpu} split {G} ways ({out['strong']['config']})"
+        if args.block == 1 and rows and not args.exchange_fp32:
+            # the same row split with the opt-in fp32 exchange (half the all-reduce bytes): with the
+            # fp64 line, the strong leg and the column split, four message sizes per SCALE run for the
+            # alpha / beta all-reduce model of DESIGN.md section 6.1
+            a2 = argparse.Namespace(**vars(args))
+            a2.exchange_fp32 = 1
+            fresh()
+            res = measure(ctx, a2, m, n_total)
+            out["rows_exchange_fp32"] = leg_summary(ctx, res, K, G, weak)
+            out["rows_exchange_fp32"]["config"] = (f"m={m} n={n_total} row-sharded, all-reduce of n+5 fp32 "
+                                                   f"({out['rows_exchange_fp32']['config']})")
         if args.block == 1 and rows:
             a2 = argparse.Namespace(**vars(args))
             a2.shard = "columns"
@@ -884,15 +896,18 @@ def main():
             if ctx.rank == 0:
                 a3 = argparse.Namespace(**vars(args))
                 a3.comm = False
-                res = measure(SoloCtx(ctx), a3, m, args.n_per_gpu)
+                solo = SoloCtx(ctx)
+                res = measure(solo, a3, m, args.n_per_gpu)
                 n1 = window_rate(res, K)[0]
+                o = leg_summary(solo, res, K, 1, False)
             ctx.barrier()
             if ctx.rank == 0:
-                o = {"value": n1, "unit": "iters/s",
-                     "config": f"m={m} n={args.n_per_gpu} on rank 0's GPU alone (no communicator), same run",
-                     "efficiency_weak_rows": out["value"] / (G * n1)}
+                o.update({"config": f"m={m} n={args.n_per_gpu} on rank 0's GPU alone (no communicator), same run",
+                          "efficiency_weak_rows": out["value"] / (G * n1)})
                 if "strong" in out:
                     o["speedup_strong_rows"] = out["strong"]["value"] / n1
+                if "rows_exchange_fp32" in out:
+                    o["efficiency_weak_rows_exchange_fp32"] = out["rows_exchange_fp32"]["value"] / (G * n1)
                 if "columns" in out:
                     o["efficiency_weak_columns"] = out["columns"]["value"] / (G * n1)
                     if "strong" in out["columns"]:

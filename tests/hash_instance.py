@@ -146,6 +146,12 @@ def np_A_bf16(m, n, chunk_rows=None):
     return A
 
 
+def np_entries_bf16(rows, cols, n):
+    """A[rows, cols] of np_A_bf16 without building A"""
+    idx = np.asarray(rows, dtype=np.int64) * n + np.asarray(cols, dtype=np.int64)
+    return ((_hash(idx, SEED_A, np) >> 24) - 128).astype(np.float32) * np.float32(bf16_scale(n))
+
+
 def torch_A_bf16(m, n, device, chunk_rows=None):
     import torch
     chunk_rows = chunk_rows or max(1, (1 << 26) // n)

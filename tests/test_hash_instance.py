@@ -20,6 +20,12 @@ def test_numpy_and_torch_agree_bitwise():
     assert np.array_equal(H.torch_b(At).numpy(), b)
     rows, cols = H.sample_points(300, 1000, k=64)
     assert np.array_equal(H.np_entries(rows, cols, 1000), A[rows, cols])
+    Ab = H.np_A_bf16(300, 1000)
+    assert torch.equal(H.torch_A_bf16(300, 1000, "cpu"), torch.from_numpy(Ab))
+    assert np.array_equal(H.np_entries_bf16(rows, cols, 1000), Ab[rows, cols])
+    assert torch.equal(torch.from_numpy(Ab).to(torch.bfloat16).float(), torch.from_numpy(Ab))   # exact in bf16
+    B = H.torch_B(torch.from_numpy(Ab), 3)
+    assert all(np.array_equal(B[:, r].numpy(), H.np_b_rhs(Ab, r)) for r in range(3))
 
 
 def test_b_is_exact_in_any_order():
@@ -37,6 +43,14 @@ def test_committed_fixtures_match_the_generator():
     for path in sorted(glob.glob(os.path.join(GOLD, "longrun_*.npz"))):
         fx = dict(np.load(path))
         n = int(fx["n"])
+        assert int(fx["iters"]) >= 260, path
+        if "rhs" in fx:   # configs[4]: bf16 A, the oracle's RHS
+            assert np.array_equal(H.np_entries_bf16(fx["A_rows"], fx["A_cols"], n), fx["A_samples"]), path
+            for r in fx["rhs"]:
+                x = fx[f"x_{r}"]
+                assert x.shape == (n,) and np.isfinite(x).all()
+                assert fx[f"err_iter_{r}"][-1] < fx[f"err_iter_{r}"][0]
+            continue
         assert np.array_equal(H.np_entries(fx["A_rows"], fx["A_cols"], n), fx["A_samples"]), path
-        assert int(fx["iters"]) >= 260 and fx["x"].shape == (n,) and np.isfinite(fx["x"]).all()
+        assert fx["x"].shape == (n,) and np.isfinite(fx["x"]).all()
         assert fx["err_iter"][-1] < fx["err_iter"][0]

@@ -2,9 +2,10 @@
 # Rehearsal of bench.py's N > 1 path on a one-GPU box: two ranks under torch.distributed.run,
 # both on device 0 (BPGL_BENCH_DEVICE=0).  Throughput numbers are meaningless; the run checks
 # that the multi-rank code path (gloo side channel, RCCL communicator, row shards, strong leg,
-# JSON line) works end to end.  Default split: columns -- the row split's k_onepass needs all of its
-# blocks co-resident, which ranks sharing one GPU cannot guarantee (it then stops with
-# BPGL_E_EXCHANGE by design); `--shard rows` may be passed and passes when the ranks interleave.
+# JSON line) works end to end.  Default split: columns -- without CU partitions the row split's
+# k_onepass cannot keep all of its blocks co-resident beside another rank's (it then falls back to
+# the two-pass row iteration by design).  tools/rehearse_cumask.sh gives every rank its own CUs and
+# runs the default row split as designed (round 3).
 # Usage (GPU box): [NPROC=N] tools/rehearse_n2.sh [extra bench args]
 set -o pipefail
 mkdir -p gpurun_out/rehearse
