@@ -212,3 +212,25 @@ def test_row_sharded_exchange_protocol_matches_reference():
     # a failure on one rank: the same iterates bit for bit, on both ranks
     np.testing.assert_array_equal(np.array(out[("failed", 0)]), np.array(out[0]))
     np.testing.assert_array_equal(np.array(out[("failed", 1)]), np.array(out[0]))
+
+
+def test_xcd_symmetric_cu_masks():
+    """distributed.xcd_symmetric_cu_mask: the ranks' masks are disjoint, cover
+    the device, and give every XCD the same number of each rank's CUs whether the driver maps mask bit i
+    to XCD i % 8 (interleaved) or to XCD i // 32 (runs) -- an XCD without CUs would never run its share of
+    a persistent grid"""
+    import pytest
+    from convex_optimization_amd.distributed import xcd_symmetric_cu_mask
+    cus = 256
+    for nranks in (1, 2, 4):
+        masks = [xcd_symmetric_cu_mask(r, nranks, cus) for r in range(nranks)]
+        bits = [{i for i in range(cus) if (m[i // 32] >> (i % 32)) & 1} for m in masks]
+        assert set().union(*bits) == set(range(cus))
+        assert sum(len(b) for b in bits) == cus                       # disjoint
+        for b in bits:
+            assert [sum(1 for i in b if i % 8 == x) for x in range(8)] == [32 // nranks] * 8
+            assert [sum(1 for i in b if i // 32 == x) for x in range(8)] == [32 // nranks] * 8
+    with pytest.raises(ValueError):
+        xcd_symmetric_cu_mask(0, 8)
+    with pytest.raises(ValueError):
+        xcd_symmetric_cu_mask(2, 2)
