@@ -124,7 +124,7 @@ struct bpgl_ctx {
     int op_rowb = 1;   // k_onepass_tail: residual update on blocks of its own ("tail_row_blocks" knob)
     // fold the U partials inside k_onepass ("onepass_fold" 1) or in k_onepass_fold / the tail (0, default:
     // the in-kernel form's write-through partials and segment barrier cost more than the launch it
-    // saves -- m = 1024 rows: k_onepass 55.0 -> 67.9 us against a 12.4 us fold; profiles/r03/fold_sweep)
+    // saves -- m = 1024 rows: k_onepass 55.0 -> 67.9 us against a 12.4 us fold; profiles/r03/fold_sweep_v1)
     int op_fold = 0;
     // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
     // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
