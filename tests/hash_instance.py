@@ -27,7 +27,7 @@ def a_scale(n):
     return 2.0 ** -round(math.log2(math.sqrt(n / 12.0)))
 
 
-def _mix(h, xp):
+def _mix(h):
     h = h ^ (h >> 16)
     h = (h * MUL1) & M32
     h = h ^ (h >> 15)
@@ -35,22 +35,22 @@ def _mix(h, xp):
     return h ^ (h >> 16)
 
 
-def _hash(idx, seed, xp):
-    return _mix(((idx & M32) * GOLD + seed) & M32, xp)
+def _hash(idx, seed):
+    return _mix(((idx & M32) * GOLD + seed) & M32)
 
 
 # ---------------------------------------------------------------- numpy (offline generator)
 def np_rows(i0, i1, n):
     """rows [i0, i1) of A as float32"""
     idx = np.arange(i0 * n, i1 * n, dtype=np.int64)
-    u = (_hash(idx, SEED_A, np) >> 8) - (1 << 23)
+    u = (_hash(idx, SEED_A) >> 8) - (1 << 23)
     return (u.astype(np.float32) * np.float32(2.0 ** -24 * a_scale(n))).reshape(i1 - i0, n)
 
 
 def np_entries(rows, cols, n):
     """A[rows, cols] without building A"""
     idx = np.asarray(rows, dtype=np.int64) * n + np.asarray(cols, dtype=np.int64)
-    u = (_hash(idx, SEED_A, np) >> 8) - (1 << 23)
+    u = (_hash(idx, SEED_A) >> 8) - (1 << 23)
     return u.astype(np.float32) * np.float32(2.0 ** -24 * a_scale(n))
 
 
@@ -64,7 +64,7 @@ def np_A(m, n, chunk_rows=None):
 
 
 def np_x_true(n):
-    h = _hash(np.arange(n, dtype=np.int64), SEED_X, np)
+    h = _hash(np.arange(n, dtype=np.int64), SEED_X)
     keep = (h & 0xFFFF) < int(0.4 * 65536)
     c = ((h >> 16) % 6).astype(np.int64)
     c = np.where(c < 3, c - 3, c - 2)          # -3, -2, -1, 1, 2, 3
@@ -72,7 +72,7 @@ def np_x_true(n):
 
 
 def np_e(m):
-    u = (_hash(np.arange(m, dtype=np.int64), SEED_E, np) >> 8) - (1 << 23)
+    u = (_hash(np.arange(m, dtype=np.int64), SEED_E) >> 8) - (1 << 23)
     return u.astype(np.float64) * 2.0 ** -34
 
 
@@ -96,7 +96,7 @@ def torch_A(m, n, device, chunk_rows=None):
     for i0 in range(0, m, chunk_rows):
         i1 = min(m, i0 + chunk_rows)
         idx = torch.arange(i0 * n, i1 * n, dtype=torch.int64, device=device)
-        u = (_hash(idx, SEED_A, torch) >> 8) - (1 << 23)
+        u = (_hash(idx, SEED_A) >> 8) - (1 << 23)
         A[i0:i1] = (u.to(torch.float32) * sc).reshape(i1 - i0, n)
     return A
 
@@ -142,14 +142,14 @@ def np_A_bf16(m, n, chunk_rows=None):
     for i0 in range(0, m, chunk_rows):
         i1 = min(m, i0 + chunk_rows)
         idx = np.arange(i0 * n, i1 * n, dtype=np.int64)
-        A[i0:i1] = (((_hash(idx, SEED_A, np) >> 24) - 128).astype(np.float32) * sc).reshape(i1 - i0, n)
+        A[i0:i1] = (((_hash(idx, SEED_A) >> 24) - 128).astype(np.float32) * sc).reshape(i1 - i0, n)
     return A
 
 
 def np_entries_bf16(rows, cols, n):
     """A[rows, cols] of np_A_bf16 without building A"""
     idx = np.asarray(rows, dtype=np.int64) * n + np.asarray(cols, dtype=np.int64)
-    return ((_hash(idx, SEED_A, np) >> 24) - 128).astype(np.float32) * np.float32(bf16_scale(n))
+    return ((_hash(idx, SEED_A) >> 24) - 128).astype(np.float32) * np.float32(bf16_scale(n))
 
 
 def torch_A_bf16(m, n, device, chunk_rows=None):
@@ -160,12 +160,12 @@ def torch_A_bf16(m, n, device, chunk_rows=None):
     for i0 in range(0, m, chunk_rows):
         i1 = min(m, i0 + chunk_rows)
         idx = torch.arange(i0 * n, i1 * n, dtype=torch.int64, device=device)
-        A[i0:i1] = (((_hash(idx, SEED_A, torch) >> 24) - 128).to(torch.float32) * sc).reshape(i1 - i0, n)
+        A[i0:i1] = (((_hash(idx, SEED_A) >> 24) - 128).to(torch.float32) * sc).reshape(i1 - i0, n)
     return A
 
 
 def np_x_true_rhs(n, r):
-    h = _hash(np.arange(n, dtype=np.int64) + np.int64(r) * n, SEED_XK, np)
+    h = _hash(np.arange(n, dtype=np.int64) + np.int64(r) * n, SEED_XK)
     keep = (h & 0xFFFF) < int(0.4 * 65536)
     c = ((h >> 16) % 6).astype(np.int64)
     c = np.where(c < 3, c - 3, c - 2)
@@ -173,7 +173,7 @@ def np_x_true_rhs(n, r):
 
 
 def np_e_rhs(m, r):
-    u = (_hash(np.arange(m, dtype=np.int64) + np.int64(r) * m, SEED_EK, np) >> 8) - (1 << 23)
+    u = (_hash(np.arange(m, dtype=np.int64) + np.int64(r) * m, SEED_EK) >> 8) - (1 << 23)
     return u.astype(np.float64) * 2.0 ** -34
 
 

@@ -352,3 +352,22 @@ def test_two_pass_row_iteration_matches_plain_solver():
         assert rel(g1["x"], ref["x"]) <= 1e-10, rel(g1["x"], ref["x"])
         T = ref["t_last"] + 1
         np.testing.assert_allclose(g1["err_iter"][:T], ref["err_iter"][:T], rtol=1e-8, atol=1e-12)
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_in_kernel_fold_rows_is_bitwise(fp32):
+    """row shards with "onepass_fold" = 1: k_onepass writes the exchange buffer itself (the column
+    sums in the same group order as k_onepass_fold, the scalars by the last block to arrive) -- the
+    same bits as the separate fold kernel, one-rank RCCL and two caller-exchange ranks"""
+    rs = np.random.RandomState(9)
+    m, n = 1500, 12000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
+    rows.set_tuning("exchange_fp32", -1 if fp32 else 0)
+    ref = rows.run(b, mu, 120)["x"]
+    rows.set_tuning("onepass_fold", 1)
+    got = rows.run(b, mu, 120)["x"]
+    assert rows.solver_stat("onepass") == 1 and rows.solver_stat("fallbacks") == 0
+    np.testing.assert_array_equal(got, ref)
