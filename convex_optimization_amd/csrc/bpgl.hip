@@ -168,7 +168,7 @@ void geometry(bpgl_ctx* c) {
                  : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<3, bf16_t>::BC;
     const int64_t SB = cdiv(c->wp, bc);
     c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
-    c->op_gpl = SB > 64 ? 2 : 1;
+    c->op_gpl = SB > 64 ? 2 : 1;   // k_onepass<..., 2> relies on SB > 64
     if (c->op_shape) {
         int64_t ng = std::min<int64_t>(std::min<int64_t>(c->cus / SB, c->m), kOpMaxGroups);
         const int64_t R = cdiv(c->m, ng);

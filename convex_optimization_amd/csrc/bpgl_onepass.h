@@ -398,10 +398,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             op_u64 v[GPL];
 #pragma unroll
             for (int k = 0; k < GPL; ++k) v[k] = gv[q][k];
+            // lanes past SB read block 0's granule (glane), which is ready exactly when block 0's is:
+            // no per-lane exemption needed (fewer VALU ops per row at one wave per SIMD)
             auto ready = [&]() {
                 bool ok = true;
 #pragma unroll
-                for (int k = 0; k < GPL; ++k) ok = ok && (lane + 64 * k >= SB || op_tag(v[k]) == tag);
+                for (int k = 0; k < GPL; ++k) ok = ok && op_tag(v[k]) == tag;
                 return ok;
             };
             if (!__all(ready())) {   // late: re-poll (drains this wave's queue; rare)
@@ -419,7 +421,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
 #pragma unroll
                 for (int k = 0; k < GPL; ++k) asm volatile("" : "+v"(v[k]));
             }
-            double x = lane < SB ? op_unstuff(v[0]) : 0.0;
+            // GPL 2 means SB > 64: every lane's first granule is a block of its own
+            double x = (GPL == 2 || lane < SB) ? op_unstuff(v[0]) : 0.0;
             if (GPL == 2) x += lane + 64 < SB ? op_unstuff(v[GPL - 1]) : 0.0;   // blocks l and l + 64, then the wave
             x = SB <= 16 ? op_lane(op_row_sum16(x), 0) : op_wave_sum(x);
             if (sb == 0 && wave == 0 && lane == 0) o.S[rowof(t2)] = x;
