@@ -120,7 +120,9 @@ def parse():
                     help="one-pass tail: residual update on blocks of its own (1, library default) or first in every block (0)")
     ap.add_argument("--onepass-variant", type=int, default=0, help="one-pass ring depth / prefetch variant (0-3)")
     ap.add_argument("--onepass-fold", type=int, default=-1, choices=[-1, 0, 1],
-                    help="one-pass U fold inside k_onepass (1, library default) or in k_onepass_fold / the tail (0)")
+                    help="one-pass U fold inside k_onepass (1) or in k_onepass_fold / the tail (0, library default)")
+    ap.add_argument("--graph-max", type=int, default=-1,
+                    help="largest hipGraph of iterations replayed (power of two; -1: library default, 64)")
     ap.add_argument("--onepass-cache", type=int, default=-1,
                     help="permille of each one-pass row group read with cache-allocating loads (-1: library default)")
     ap.add_argument("--comm", action="store_true",
@@ -299,6 +301,8 @@ def measure(ctx, args, m, n_total):
         gc.set_tuning("onepass_cache_permille", args.onepass_cache)
     if args.onepass_fold >= 0:
         gc.set_tuning("onepass_fold", args.onepass_fold)
+    if args.graph_max > 0:
+        gc.set_tuning("graph_max", args.graph_max)
 
     def sync():
         gc.stream.synchronize()

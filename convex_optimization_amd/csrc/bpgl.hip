@@ -89,8 +89,10 @@ struct bpgl_ctx {
     bool external = false;   // nranks > 1 with the exchange done by the caller
     // solver
     bool solver = false, use_graph = false;
-    hipGraphExec_t gexec = nullptr;     // one iteration
-    hipGraphExec_t gexec_k = nullptr;   // kGraphIters iterations (amortises the per-replay gap)
+    // gexec[j]: a hipGraph of 2^j iterations, j < kGraphLevels, 2^j <= graph_max; a run of n iterations
+    // replays the largest that fits (one replay gap per graph, not per 8 iterations)
+    hipGraphExec_t gexec[kGraphLevels] = {};
+    int graph_max = kGraphMaxIters;   // "graph_max" knob (RCCL contexts cap it at kGraphIters)
     // timing
     bool timing = false;
     std::vector<hipEvent_t> evs;   // 2 events per (timed iteration, kind)
@@ -143,8 +145,8 @@ struct bpgl_ctx {
 namespace {
 
 void drop_graphs(bpgl_ctx* c) {
-    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-    if (c->gexec_k) { (void)hipGraphExecDestroy(c->gexec_k); c->gexec_k = nullptr; }
+    for (auto& g : c->gexec)
+        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
 }
 
 void geometry(bpgl_ctx* c) {
@@ -699,23 +701,27 @@ int enqueue_iteration(bpgl_ctx* c, int64_t it) {
     return enqueue_phase(c, it, 1);
 }
 
-// hipGraphs of 1 and kGraphIters iterations (c->use_graph), uploaded to the device here so the
-// first replay inside a caller's timed region pays no upload
+// largest graph a context captures: RCCL contexts keep kGraphIters (each captured iteration holds
+// an all-reduce node), the others graph_max
+int graph_cap(const bpgl_ctx* c) { return c->comm ? std::min(c->graph_max, kGraphIters) : c->graph_max; }
+
+// hipGraphs of 1, 2, 4, ... graph_cap iterations (c->use_graph), uploaded to the device here so
+// the first replay inside a caller's timed region pays no upload
 int capture_graphs(bpgl_ctx* c) {
     drop_graphs(c);
     if (!c->use_graph) return 0;
     int rc = 0;
     const bool was_timing = c->timing;
     c->timing = false;
-    for (int variant = 0; variant < 2 && !rc; ++variant) {
-        const int iters = variant == 0 ? 1 : kGraphIters;
+    for (int level = 0; level < kGraphLevels && (1 << level) <= graph_cap(c) && !rc; ++level) {
+        const int iters = 1 << level;
         hipGraph_t graph = nullptr;
         HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         for (int k = 0; k < iters && !rc; ++k) rc = enqueue_iteration(c, 0);
         hipError_t ec = hipStreamEndCapture(c->stream, &graph);
         if (rc) { if (graph) (void)hipGraphDestroy(graph); break; }
         if (ec != hipSuccess) { rc = fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec)); break; }
-        hipGraphExec_t* dst = variant == 0 ? &c->gexec : &c->gexec_k;
+        hipGraphExec_t* dst = &c->gexec[level];
         hipError_t ei = hipGraphInstantiate(dst, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) { rc = fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei)); break; }
@@ -740,14 +746,16 @@ int step_impl(bpgl_ctx* c, int64_t n_iter) {
         }
         const int64_t room = K > 0 ? std::min<int64_t>(n_iter - i, K - c->op_t % K) : n_iter - i;
         int64_t k = 1;
-        if (!c->timing && c->gexec_k && room >= kGraphIters) {
-            HIP_TRY(hipGraphLaunch(c->gexec_k, c->stream));
-            k = kGraphIters;
-        } else if (c->timing || !c->gexec) {
+        int level = -1;   // the largest captured graph that fits the room
+        if (!c->timing)
+            for (int j = kGraphLevels - 1; j >= 0 && level < 0; --j)
+                if (c->gexec[j] && room >= (int64_t(1) << j)) level = j;
+        if (level >= 0) {
+            HIP_TRY(hipGraphLaunch(c->gexec[level], c->stream));
+            k = int64_t(1) << level;
+        } else {
             if ((rc = enqueue_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
             if (c->timing) c->timed_iters++;
-        } else {
-            HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
         }
         i += k;
         c->op_t += k;
@@ -1345,6 +1353,14 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "onepass_refresh")) {
         if (value < 0) return fail(BPGL_E_ARG, "onepass_refresh must be >= 0");
         c->op_refresh = (int)std::min<int64_t>(value, 1 << 30);
+        return 0;
+    }
+    if (!strcmp(key, "graph_max")) {   // speed only: the largest hipGraph of iterations (replays per run)
+        if (value < 1 || value > kGraphMaxIters || (value & (value - 1)))
+            return fail(BPGL_E_ARG, "graph_max must be a power of two in [1, %d]", kGraphMaxIters);
+        c->graph_max = (int)value;
+        drop_graphs(c);
+        c->solver = false;
         return 0;
     }
     if (!strcmp(key, "nt_loads")) {

@@ -27,7 +27,11 @@ struct Carve {
     }
 };
 
-constexpr int kGraphIters = 8;   // iterations captured per replayed hipGraph
+constexpr int kGraphIters = 8;   // iterations captured per replayed hipGraph (panel; RCCL contexts' cap)
+// single-RHS solver: hipGraphs of 1, 2, 4, ..., kGraphMaxIters iterations, so a run of n iterations
+// costs about log2(n) replays instead of n / 8
+constexpr int kGraphLevels = 7;
+constexpr int kGraphMaxIters = 1 << (kGraphLevels - 1);
 }  // namespace bpgl_host
 
 #define HIP_TRY(expr)                                                                        \

@@ -186,8 +186,9 @@ double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
  *   the ERR_BOUND stopping rule of lasso.py:141-150), err_iter / time_iter
  *   (device fp64, NULL = not recorded; record_len entries of err_iter and
  *   record_len + 1 of time_iter, as lasso.py:54-62).
- * bpgl_solver_step: enqueue n_iter more iterations (asynchronous; replays a
- *   captured hipGraph of one iteration when `use_graph` was set).
+ * bpgl_solver_step: enqueue n_iter more iterations (asynchronous; with
+ *   `use_graph`, replays of the captured hipGraphs of 1, 2, 4, ... iterations,
+ *   the largest that fits each time -- tuning key "graph_max").
  * bpgl_solver_status: synchronise the stream and read (iterations done,
  *   stopped flag, last t, last step size, last error).  It also completes
  *   iterations a one-pass launch lost: a launch whose blocks were not all
@@ -248,6 +249,8 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   "reverse_rows" (default 0): the A D pass walks each row chunk bottom-up.
  *   "tail_row_blocks" (default 1): the one-pass tail runs the residual update on
  *   blocks of its own, beside its column blocks (0: every block first).
+ *   "graph_max" (default 64; a power of two, at most 8 with an RCCL communicator):
+ *   the largest hipGraph of iterations bpgl_solver_reset captures (use_graph).
  * These select the iteration's arithmetic path (results agree to rounding,
  * each path is bitwise deterministic):
  *   "onepass" (default -1 = when eligible, 0 = off, 1 = required): one pass

@@ -118,6 +118,31 @@ def test_graph_eager_split_steps_bitwise():
     np.testing.assert_array_equal(gc.solver_x(), gc.run(b, mu, 90)["x"])
 
 
+@pytest.mark.parametrize("graph_max", [1, 2, 8, 64])
+def test_graph_sizes_bitwise(graph_max):
+    """hipGraphs of 1, 2, ... graph_max iterations: only the replay count changes"""
+    rs = np.random.RandomState(11)
+    A = rs.randn(700, 6000)
+    b = rs.randn(700)
+    gc = make_cls("float")(A, 1, device=0)
+    mu = 0.05 * float(np.abs(A.T @ b).max())
+    gc.set_tuning("onepass_refresh", 64)
+    e = gc.run(b, mu, 150, use_graph=False)["x"]
+    gc.set_tuning("graph_max", graph_max)
+    gc.solver_reset(b, mu)
+    for k in (1, 20, 63, 2, 64):   # 150 iterations in runs that straddle the refreshes at 64 and 128
+        gc.solver_step(k)
+    np.testing.assert_array_equal(gc.solver_x(), e)
+    assert gc.solver_stat("enqueued") == 150 and gc.solver_stat("refreshes") == 2
+
+
+def test_graph_max_rejects_bad_values():
+    gc = make_cls("float")(np.ones((64, 256)), 1, device=0)
+    for v in (0, 3, 128, -1):
+        with pytest.raises(RuntimeError):
+            gc.set_tuning("graph_max", v)
+
+
 @pytest.mark.parametrize("m", [900, 3001])
 def test_tail_row_blocks_bitwise_neutral(m):
     """where k_onepass_tail runs the residual update (blocks of its own, the default, or every block
