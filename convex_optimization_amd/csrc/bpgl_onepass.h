@@ -457,8 +457,25 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         // wave wrote (fixed order: lanes stride the rows, then the wave sum) -> parts2[grp]
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __threadfence_block();
+        // 8 rows per lane in flight, then their FMAs in row order (the same bits as one row at a
+        // time; the compiler had waited for each row's two loads, a memory round trip per 64 rows
+        // on the launch's critical path)
         double rs = 0.0, ss = 0.0;
-        for (int i = lane; i < nrows; i += 64) {
+        int i = lane;
+        for (; i + 7 * 64 < nrows; i += 8 * 64) {
+            double sv[8], rv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                sv[k] = o.S[i0 + i + 64 * k];
+                rv[k] = p.r[i0 + i + 64 * k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                rs = fma(rv[k], sv[k], rs);
+                ss = fma(sv[k], sv[k], ss);
+            }
+        }
+        for (; i < nrows; i += 64) {
             const double sv = o.S[i0 + i];
             rs = fma(p.r[i0 + i], sv, rs);
             ss = fma(sv, sv, ss);
