@@ -121,8 +121,6 @@ def parse():
     ap.add_argument("--onepass-variant", type=int, default=0, help="one-pass ring depth / prefetch variant (0-3)")
     ap.add_argument("--onepass-fold", type=int, default=-1, choices=[-1, 0, 1],
                     help="one-pass U fold inside k_onepass (1) or in k_onepass_fold / the tail (0, library default)")
-    ap.add_argument("--tail-fuse", type=int, default=-1, choices=[-1, 0, 1],
-                    help="one rank: the one-pass tail inside the next k_onepass (1) or its own launch (0); -1: library default")
     ap.add_argument("--graph-max", type=int, default=-1,
                     help="largest hipGraph of iterations replayed (power of two; -1: library default, 64)")
     ap.add_argument("--onepass-cache", type=int, default=-1,
@@ -305,8 +303,6 @@ def measure(ctx, args, m, n_total):
         gc.set_tuning("onepass_fold", args.onepass_fold)
     if args.graph_max > 0:
         gc.set_tuning("graph_max", args.graph_max)
-    if args.tail_fuse >= 0:
-        gc.set_tuning("tail_fuse", args.tail_fuse)
 
     def sync():
         gc.stream.synchronize()

@@ -42,7 +42,6 @@ using namespace bpgl_host;
 
 namespace {
 constexpr int kTimedKinds = 9;   // + 8: the exact-gradient refresh of the one-pass iteration
-constexpr int kFlushKind = 9;    // ev_record only: the fused tail's flush (reported inside kind 6)
 constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
@@ -99,8 +98,6 @@ struct bpgl_ctx {
     std::vector<hipEvent_t> evs;   // 2 events per (timed iteration, kind)
     std::vector<hipEvent_t> ref_evs;   // 2 events per timed exact-gradient refresh (kind 8)
     int64_t ref_timed = 0;
-    std::vector<hipEvent_t> fl_evs;    // 2 events per timed fused-tail flush (amortised into kind 6)
-    int64_t fl_timed = 0;
     int64_t timed_iters = 0;
     bool kind_used[kTimedKinds] = {};
     double wall_tick_s = 1e-8;
@@ -131,9 +128,6 @@ struct bpgl_ctx {
     // the in-kernel form's write-through partials and segment barrier cost more than the launch it
     // saves -- m = 1024 rows: k_onepass 55.0 -> 67.9 us against a 12.4 us fold; profiles/r03/fold_sweep_v1)
     int op_fold = 0;
-    // fused tail ("tail_fuse"): one rank's k_onepass applies the previous iteration's update in a
-    // prologue instead of a k_onepass_tail launch (bpgl_onepass.h, OnePassArgs::fuse)
-    int tail_fuse = 0;
     // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
     // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
     bool rows = false;
@@ -155,12 +149,6 @@ void drop_graphs(bpgl_ctx* c) {
         if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
 }
 
-// columns per one-pass segment block (OnePassGeo<OpLU<T>::LU, T>::BC)
-int op_bc(const bpgl_ctx* c) {
-    return c->dtype == BPGL_F32 ? OnePassGeo<4, float>::BC
-         : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<3, bf16_t>::BC;
-}
-
 void geometry(bpgl_ctx* c) {
     const int V = vec_elems(c->dtype);
     c->segw = 64 * V * kU;
@@ -178,7 +166,9 @@ void geometry(bpgl_ctx* c) {
     c->nchunk = (int)cdiv(c->m, R);
     c->nparts = (int)cdiv(c->wp, kColsPerShrink);
     // one-pass geometry: SB segment blocks per row, floor(CUs / SB) row groups, one block per CU
-    const int64_t SB = cdiv(c->wp, op_bc(c));
+    const int bc = c->dtype == BPGL_F32 ? OnePassGeo<4, float>::BC
+                 : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<3, bf16_t>::BC;
+    const int64_t SB = cdiv(c->wp, bc);
     c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
     c->op_gpl = SB > 64 ? 2 : 1;   // k_onepass<..., 2> relies on SB > 64
     if (c->op_shape) {
@@ -222,7 +212,7 @@ Layout layout(const bpgl_ctx* c) {
     L.slab_s = k.take(8 * (int64_t)c->nseg * c->m);
     L.g = k.take(8 * c->wp);
     L.D = k.take(8 * c->wp);
-    L.parts = k.take(8 * 4 * std::max<int64_t>(std::max(c->nparts, c->op_tail_grid), (int64_t)c->op_ngroups * c->op_SB));
+    L.parts = k.take(8 * 4 * (int64_t)std::max(c->nparts, c->op_tail_grid));
     L.parts2 = k.take(8 * 2 * std::max<int64_t>(kMaxReduceBlocks, c->nchunk));
     L.Dbuf = k.take(8 * 2 * c->wp);
     L.cnt = k.take(8 * ((int64_t)c->nseg + c->nchunk));
@@ -361,8 +351,7 @@ Params op_params(const bpgl_ctx* c) {
     q.slab_g = c->op.G;
     q.nchunk = 1;
     q.nseg = 1;
-    // shrink partials come from k_onepass_tail, or (fused tail) one per k_onepass block
-    q.nparts = c->op.fuse ? c->op_ngroups * c->op_SB : c->op_tail_grid;
+    q.nparts = c->op_tail_grid;   // shrink partials come from k_onepass_tail
     return q;
 }
 // GPL: granules per lane of the row hand-off (SB <= 64: 1, SB <= 128: 2)
@@ -440,16 +429,6 @@ void op_configure(bpgl_ctx* c) {
     c->op.fold = c->op_on && c->op_fold ? 1 : 0;
     c->op.rows_out = c->rows && c->op.fold ? 1 : 0;
     c->op.Ufold32 = c->op.fold && xch_f32(c) ? reinterpret_cast<float*>(c->p.comm) : nullptr;
-    c->op.fuse = c->op_on && c->tail_fuse && !c->rows && !c->comm && !c->external && !c->op.fold ? 1 : 0;
-}
-// the fused tail's slices as their own launch (k_onepass's grid): UPDATE = the flush of a pending
-// update, !UPDATE = the shrink after a reset or refresh
-template <bool UPDATE>
-int onepass_slices(bpgl_ctx* c) {
-    hipLaunchKernelGGL(k_onepass_slices<UPDATE>, dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0,
-                       c->stream, op_params(c), c->op, op_bc(c));
-    LAUNCH_CHECK("k_onepass_slices");
-    return 0;
 }
 template <bool UPDATE>
 int onepass_tail(bpgl_ctx* c) {
@@ -480,8 +459,7 @@ int onepass_refresh(bpgl_ctx* c) {
     int rc;
     if ((rc = onepass_local_gradient(c, c->op.G))) return rc;
     if (c->rows && c->comm && (rc = allreduce_sum(c, c->op.G, c->wp))) return rc;
-    // the shrink of the next iteration from the exact g
-    return c->op.fuse ? onepass_slices<false>(c) : onepass_tail<false>(c);
+    return onepass_tail<false>(c);   // the shrink of the next iteration from the exact g
 }
 // can this solver run use the one-pass iteration?  (0 yes; else the reason)
 const char* onepass_ineligible(bpgl_ctx* c) {
@@ -507,18 +485,16 @@ int check_ready(const bpgl_ctx* c) {
 // iteration) has its own event list, 2 per refresh.
 void ev_record(bpgl_ctx* c, int64_t it, int kind, int end) {
     if (!c->timing) return;
-    if (kind == 8 || kind == kFlushKind) {   // not in every iteration: lists of their own
-        std::vector<hipEvent_t>& evs = kind == 8 ? c->ref_evs : c->fl_evs;
-        int64_t& n = kind == 8 ? c->ref_timed : c->fl_timed;
-        const size_t idx = 2 * (size_t)n + end;
-        while (evs.size() <= idx) {
+    if (kind == 8) {
+        const size_t idx = 2 * (size_t)c->ref_timed + end;
+        while (c->ref_evs.size() <= idx) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return;
-            evs.push_back(e);
+            c->ref_evs.push_back(e);
         }
-        (void)hipEventRecord(evs[idx], c->stream);
-        if (end) n++;
-        if (kind == 8) c->kind_used[kind] = true;
+        (void)hipEventRecord(c->ref_evs[idx], c->stream);
+        if (end) c->ref_timed++;
+        c->kind_used[kind] = true;
         return;
     }
     const size_t idx = 2 * ((size_t)it * kTimedKinds + kind) + end;
@@ -663,7 +639,7 @@ int enqueue_phase_onepass(bpgl_ctx* c, int64_t it, int phase) {
         ev_record(c, it, 7, 0);
         if ((rc = onepass_launch(c))) return rc;
         ev_record(c, it, 7, 1);
-    } else if (!c->op.fuse) {   // fused tail: the next k_onepass (or the flush) applies the update
+    } else {
         ev_record(c, it, 6, 0);
         if ((rc = onepass_tail<true>(c))) return rc;
         ev_record(c, it, 6, 1);
@@ -756,25 +732,13 @@ int capture_graphs(bpgl_ctx* c) {
     return rc;
 }
 
-// fused tail: apply a pending update with a launch of its own (its time is amortised over the
-// window's iterations into the "update" kind, which the fused iteration leaves unused)
-int onepass_flush(bpgl_ctx* c) {
-    int rc;
-    ev_record(c, 0, kFlushKind, 0);
-    if ((rc = onepass_slices<true>(c))) return rc;
-    ev_record(c, 0, kFlushKind, 1);
-    return 0;
-}
-
 // enqueue n_iter iterations (graph replays when captured), with the one-pass exact-gradient
-// refresh every op_refresh iterations; with the fused tail the update of the last iteration is
-// applied before a refresh and at the end (so x, r and the records are current between calls)
+// refresh every op_refresh iterations
 int step_impl(bpgl_ctx* c, int64_t n_iter) {
     int rc;
     const int64_t K = c->op_on ? c->op_refresh : 0;
     for (int64_t i = 0; i < n_iter;) {
         if (K > 0 && c->op_t > 0 && c->op_t % K == 0) {
-            if (c->op.fuse && (rc = onepass_flush(c))) return rc;
             ev_record(c, c->timed_iters, 8, 0);
             c->n_refresh++;
             if ((rc = onepass_refresh(c))) return rc;
@@ -796,7 +760,6 @@ int step_impl(bpgl_ctx* c, int64_t n_iter) {
         i += k;
         c->op_t += k;
     }
-    if (c->op_on && c->op.fuse && n_iter > 0 && (rc = onepass_flush(c))) return rc;
     return finalize_fused(c);
 }
 
@@ -924,7 +887,6 @@ void bpgl_destroy(bpgl_ctx* c) {
     drop_graphs(c);
     for (auto e : c->evs) (void)hipEventDestroy(e);
     for (auto e : c->ref_evs) (void)hipEventDestroy(e);
-    for (auto e : c->fl_evs) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1393,13 +1355,6 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->op_refresh = (int)std::min<int64_t>(value, 1 << 30);
         return 0;
     }
-    if (!strcmp(key, "tail_fuse")) {   // one rank: the one-pass tail inside the next k_onepass (results agree to rounding)
-        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "tail_fuse must be 0 or 1");
-        c->tail_fuse = (int)value;
-        drop_graphs(c);
-        c->solver = false;
-        return 0;
-    }
     if (!strcmp(key, "graph_max")) {   // speed only: the largest hipGraph of iterations (replays per run)
         if (value < 1 || value > kGraphMaxIters || (value & (value - 1)))
             return fail(BPGL_E_ARG, "graph_max must be a power of two in [1, %d]", kGraphMaxIters);
@@ -1422,7 +1377,6 @@ int bpgl_set_kernel_timing(bpgl_ctx* c, int enable) {
     c->timing = enable != 0;
     c->timed_iters = 0;
     c->ref_timed = 0;
-    c->fl_timed = 0;
     for (int k = 0; k < kTimedKinds; ++k) c->kind_used[k] = false;
     return 0;
 }
@@ -1436,11 +1390,6 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, c->ref_evs[2 * r], c->ref_evs[2 * r + 1]));
         sum[8] += ms;
-    }
-    for (int64_t r = 0; r < c->fl_timed; ++r) {   // fused-tail flushes, amortised like the refresh
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, c->fl_evs[2 * r], c->fl_evs[2 * r + 1]));
-        sum[6] += ms;
     }
     for (int64_t it = 0; it < c->timed_iters; ++it) {
         for (int k = 0; k < kTimedKinds - 1; ++k) {
@@ -1456,7 +1405,6 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
     if (samples) *samples = c->timed_iters;
     c->timed_iters = 0;
     c->ref_timed = 0;
-    c->fl_timed = 0;
     for (int k = 0; k < kTimedKinds; ++k) c->kind_used[k] = false;
     return 0;
 }

@@ -45,11 +45,6 @@ struct DevState {
     long long op_fail;    // one-pass mode: a hand-off poll ran out (blocks not co-resident)
     unsigned long long op_cnt;   // one-pass mode: row-group arrivals (k_onepass line search)
     long long op_base;    // one-pass mode: op_epoch at the solver reset (row direction = parity since)
-    // one-pass fused tail ("tail_fuse"): the update of iteration tail_t - 1 (x, Ax, r, g += gamma U and
-    // the next shrink) is pending before iteration tail_t unless tail_applied == tail_t; the next
-    // k_onepass applies it in its prologue, or k_onepass_slices (the flush) does
-    long long tail_t;
-    long long tail_applied;
 };
 
 struct Params {
@@ -561,20 +556,16 @@ __device__ __forceinline__ double bld1_sc1(__amdgpu_buffer_rsrc_t r, long long o
 }
 
 // fold the shrink partials (fixed order) : sum |Bx|, sum |x|, max err
-// SC1: the partials were written (write-through) by other blocks of the running launch (the
-// one-pass fused tail): read them past the XCD-local L2s
-template <bool SC1 = false>
 __device__ void fold_parts(const Params& p, int count, double& a, double& b, double& e) {
     __shared__ double sred[3][kWaves];
     a = 0.0; b = 0.0; e = 0.0;
     int k = threadIdx.x;
-    auto ld = [&](long long i) { return SC1 ? ld_sc1(p.parts + i) : p.parts[i]; };
     for (; k + 3 * kThreads < count; k += 4 * kThreads) {   // 4 partials' loads in flight, adds in order
         double v[4][3];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) v[u][c] = ld(4ll * (k + u * kThreads) + c);
+            for (int c = 0; c < 3; ++c) v[u][c] = p.parts[4ll * (k + u * kThreads) + c];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             a += v[u][0];
@@ -583,9 +574,9 @@ __device__ void fold_parts(const Params& p, int count, double& a, double& b, dou
         }
     }
     for (; k < count; k += kThreads) {
-        a += ld(4ll * k);
-        b += ld(4ll * k + 1);
-        const double ek = ld(4ll * k + 2);
+        a += p.parts[4ll * k];
+        b += p.parts[4ll * k + 1];
+        const double ek = p.parts[4ll * k + 2];
         e = (ek > e || ek != ek) ? ek : e;
     }
     a = wave_sum(a);
@@ -768,8 +759,6 @@ __global__ __launch_bounds__(kThreads) void k_reset(Params p) {
         st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0; st->pending = 0;
         st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0; st->op_fail = 0;
         st->op_cnt = 0;
-        st->tail_t = 0;
-        st->tail_applied = 0;
         st->op_base = st->op_epoch;
         st->t_base = (long long)wall_clock64();
         if (p.time_iter) p.time_iter[0] = 0.0;

@@ -75,12 +75,6 @@ struct OnePassArgs {
     double* Ufold;               // [wp] the folded U (one rank: read by the tail; rows: the exchange buffer)
     float* Ufold32;              // rows, fp32 exchange: the folded U as fp32 (instead of Ufold)
     int rows_out;                // rows: the last block to arrive writes [r.s23 | s23.s23 | failed] and abe
-    // fused tail ("tail_fuse" = 1, one rank): no k_onepass_tail launch -- k_onepass applies the previous
-    // iteration's update in a prologue (op_slice: block (grp, sb) owns slice grp of segment sb's columns
-    // and, for sb = 0, its group's rows), the segment's ngroups blocks meet at segcnt[sb], then stream;
-    // k_onepass_slices runs the same slices as a launch of its own (before a refresh, at the end of a
-    // bpgl_solver_step, and the shrink after a reset / refresh)
-    int fuse;
 };
 
 typedef unsigned long long op_u64;
@@ -163,13 +157,7 @@ __device__ __forceinline__ bool op_arrive_last(unsigned long long* cnt, unsigned
     __syncthreads();
     return last != 0;
 }
-// the fused tail's bookkeeping at the last arrival of a launch that may have applied it (its
-// prologue, or k_onepass_slices): the iterations done include the update of tail_t - 1
-__device__ __forceinline__ void op_tail_applied(DevState* st) {
-    if (st->tail_applied != st->tail_t) st->iters = st->tail_t;
-    st->tail_applied = st->tail_t;
-}
-__device__ void op_linesearch(const Params& p, int ngroups, int fuse) {
+__device__ void op_linesearch(const Params& p, int ngroups) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double rs = 0.0, ss = 0.0;
     for (int k = threadIdx.x; k < ngroups; k += kThreads) {
@@ -184,20 +172,9 @@ __device__ void op_linesearch(const Params& p, int ngroups, int fuse) {
     rs = ((sr[0] + sr[1]) + sr[2]) + sr[3];
     ss = ((sq[0] + sq[1]) + sq[2]) + sq[3];
     double a, b, e;
-    if (fuse) fold_parts<true>(p, p.nparts, a, b, e);   // this launch's prologue wrote them
-    else fold_parts(p, p.nparts, a, b, e);
-    if (threadIdx.x == 0) {
-        DevState* st = p.st;
-        if (fuse) {
-            op_tail_applied(st);
-            st->op_epoch = st->op_epoch + 1;   // every block read it at its start (k_onepass_tail's job otherwise)
-        }
-        // every block set op_fail (if it failed) before it arrived: a failed launch commits nothing
-        if (!op_failed(p)) {
-            finish_step(p, rs, ss, a, b, e);
-            if (fuse && !st->done) st->tail_t = st->t;   // this iteration's update is now pending
-        }
-    }
+    fold_parts(p, p.nparts, a, b, e);
+    // every block set op_fail (if it failed) before it arrived: a failed launch commits nothing
+    if (threadIdx.x == 0 && !op_failed(p)) finish_step(p, rs, ss, a, b, e);
 }
 
 // Row shards, in-kernel fold: the last block of the launch to arrive writes the exchange tail
@@ -279,129 +256,6 @@ __device__ bool op_fold_segment(const Params& p, const OnePassArgs& o, int grp, 
     return true;
 }
 
-// ---------------------------------------------------------------------------
-// Fused tail (o.fuse, one rank).  State words the decision reads are written only by earlier
-// launches or by the last block to arrive (after every block has read them), so the decision is
-// grid-uniform; op_fail is left out on purpose (a failing block of the running launch sets it).
-// tail_t == t holds throughout (reset: both 0; a successful line search advances both).
-__device__ __forceinline__ bool op_tail_pending(const Params& p) {
-    const DevState* st = p.st;
-    return st->done == 0 && st->tail_applied != st->tail_t;
-}
-
-// One slice of the fused tail: columns [c0, c1) -- slice grp of segment sb's BC columns -- and, for
-// sb = 0, the rows of row group grp.  UPDATE: g += gamma sum_q U_q (q = 0, 1, ... in order; 8 loads
-// in flight), x += gamma D, Ax += gamma s23, r = Ax - b (lasso.py:153-155, :105); then the next
-// shrink (lasso.py:114-119, cpu_calculation.py:15-20): D, g mirrored to p.g, and this block's
-// [sum|Bx|, sum|x|, max err] in parts[grp * SB + sb] (the line search folds them, lasso.py:129-131).
-// WT: D and the partials written through (read by other blocks of the running launch).
-template <bool UPDATE, bool WT>
-__device__ void op_slice(const Params& p, const OnePassArgs& o, int grp, int sb, int BC, double gamma) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int per = (BC + o.ngroups - 1) / o.ngroups;
-    const long long s0 = (long long)sb * BC;
-    const long long send = s0 + BC < p.wp ? s0 + BC : p.wp;
-    const long long c0 = s0 + (long long)grp * per;
-    const long long c1 = c0 + per < send ? c0 + per : send;
-    if (UPDATE && sb == 0) {   // this row group's residual rows
-        const long long i0 = (long long)grp * o.R;
-        const long long i1 = i0 + o.R < p.m ? i0 + o.R : p.m;
-        // s23 read past the vector L1: in the prologue this block rewrites these rows of S later in
-        // the same launch and reads them back at its end
-        for (long long i = i0 + threadIdx.x; i < i1; i += kThreads) {
-            const double ax = p.Ax[i] + gamma * ld_sc1(o.S + i);
-            p.Ax[i] = ax;
-            p.r[i] = ax - p.b[i];
-        }
-    }
-    if (UPDATE && grp == 0 && sb == 0 && threadIdx.x == 0) {   // the update of iteration t - 1 completes
-        const long long t = p.st->t;
-        if (p.time_iter && t - 1 < p.rec_len)
-            p.time_iter[t] = (double)(wall_clock64() - p.st->t_base) * p.wall_tick_s;
-    }
-    double abx = 0.0, ax1 = 0.0, err = 0.0;
-    for (long long j = c0 + threadIdx.x; j < c1; j += kThreads) {
-        double g = o.G[j];
-        if (UPDATE) {
-            double u = 0.0;
-            int q = 0;
-            for (; q + 8 <= o.ngroups; q += 8) {
-                double v[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = o.Us[(long long)(q + k) * p.wp + j];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) u += v[k];
-            }
-            for (; q < o.ngroups; ++q) u += o.Us[(long long)q * p.wp + j];
-            g += gamma * u;
-            o.G[j] = g;
-        }
-        p.g[j] = g;
-        double Dj = 0.0;
-        if (j < p.w) {
-            double xj = p.x[j];
-            if (UPDATE) {
-                xj += gamma * p.D[j];
-                p.x[j] = xj;
-            }
-            const double rx = p.diag[j] * xj - g;                    // lasso.py:114
-            const double bx = p.rec[j] * soft_thr(rx, p.mu);         // lasso.py:115-117
-            Dj = bx - xj;                                            // lasso.py:119
-            abx += fabs(bx);
-            ax1 += fabs(xj);
-            const double e = fabs(g - proj(g - xj, -p.mu, p.mu));    // cpu_calculation.py:15-20
-            err = (e > err || e != e) ? e : err;
-        }
-        if (WT) st_sc1(p.D + j, Dj);
-        else p.D[j] = Dj;
-    }
-    abx = wave_sum(abx);
-    ax1 = wave_sum(ax1);
-    err = wave_max(err);
-    __shared__ double sred[3][kWaves];
-    if (lane == 0) { sred[0][wave] = abx; sred[1][wave] = ax1; sred[2][wave] = err; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        abx = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
-        ax1 = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
-        err = sred[2][0];
-        for (int q = 1; q < kWaves; ++q) err = (sred[2][q] > err || sred[2][q] != sred[2][q]) ? sred[2][q] : err;
-        double* dst = p.parts + 4ll * ((long long)grp * o.SB + sb);
-        if (WT) {
-            st_sc1(dst, abx);
-            st_sc1(dst + 1, ax1);
-            st_sc1(dst + 2, err);
-        } else {
-            dst[0] = abx;
-            dst[1] = ax1;
-            dst[2] = err;
-        }
-    }
-}
-
-// the ngroups blocks of segment sb meet (monotone counter, + ngroups per launch that runs a
-// prologue); bounded like the row hand-off.  Returns false when the wait ran out.
-__device__ bool op_seg_barrier(const OnePassArgs& o, int sb) {
-    __shared__ int seg_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's slice (D, partials) has landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long* c = o.segcnt + sb;
-        const unsigned long long ng = (unsigned long long)o.ngroups;
-        const unsigned long long old = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long target = (old / ng + 1) * ng;
-        unsigned n = kOpPolls;
-        int ok = 1;
-        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (n-- == 0) { ok = 0; break; }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        seg_ok = ok;
-    }
-    __syncthreads();
-    return seg_ok != 0;
-}
-
 template <int LU, typename T>
 struct OnePassGeo {
     static constexpr int N = VecT<T>::N;
@@ -434,13 +288,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     const bool rev = ((p.st->op_epoch - p.st->op_base) & 1) != 0;   // per solver run: reruns repeat bits
     auto rowof = [&](int t) -> long long { return rev ? i1 - 1 - t : i0 + t; };
     const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
-    // fused tail: this launch first applies the previous iteration's update (grid-uniform decision)
-    const bool fused_pro = o.fuse && op_tail_pending(p);
     if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
-        if (fused_pro) {
-            op_slice<true, true>(p, o, grp, sb, G::BC, p.st->gamma);
-            if (!op_seg_barrier(o, sb) && threadIdx.x == 0) atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
-        }
         if (sb == 0 && threadIdx.x == 0) { st_sc1(p.parts2 + 2ll * grp, 0.0); st_sc1(p.parts2 + 2ll * grp + 1, 0.0); }
         if (o.fold) {
             const __amdgpu_buffer_rsrc_t ru = rsrc(o.Us + (long long)grp * p.wp, 8ll * p.wp);
@@ -450,13 +298,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
                 atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
         }
         if ((o.ls || o.rows_out) && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) {
-            if (o.ls) op_linesearch(p, o.ngroups, o.fuse);
+            if (o.ls) op_linesearch(p, o.ngroups);
             else op_rows_scalars(p, o);
         }
         return;
     }
     const unsigned tag = (unsigned)((p.st->op_epoch + 1) & 1);   // bound scratch is zero: parity 0 = unwritten
-    if (!o.fuse && b == 0 && threadIdx.x == 0) p.st->op_ran = 1;   // fused: the last arrival advances the epoch
+    if (b == 0 && threadIdx.x == 0) p.st->op_ran = 1;
 
     for (int k = threadIdx.x; k < kOpSlots * kWaves; k += kThreads) (&part[0][0])[k] = 1ull;   // rows 0..31: parity 0
     __syncthreads();
@@ -473,7 +321,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         colok[k] = c < p.wp;
         col[k] = colok[k] ? c : 0;
 #pragma unroll
-        for (int e = 0; e < N; ++e) u[k][e] = 0.0;
+        for (int e = 0; e < N; ++e) {
+            d[k][e] = colok[k] ? p.D[c + e] : 0.0;
+            u[k][e] = 0.0;
+        }
     }
     static_assert(GPL == 1 || GPL == 2, "granules per lane");
     int glane[GPL];   // granule k of this lane: segment block lane + 64 k
@@ -589,18 +440,6 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     using NToff = std::integral_constant<bool, false>;
 #pragma unroll
     for (int q = 0; q < PF; ++q) { gload(q, q); load(NTon{}, q, q); }
-    // fused tail (after the first rows' loads, which land meanwhile): this block's slice of the
-    // previous iteration's update and the next shrink, then the segment's row groups meet, so the
-    // segment's D is complete -- read past the L2 (other XCDs wrote it through)
-    if (fused_pro) {
-        op_slice<true, true>(p, o, grp, sb, G::BC, p.st->gamma);
-        if (!op_seg_barrier(o, sb)) failed = true;   // block-uniform; the launch then commits nothing
-    }
-#pragma unroll
-    for (int k = 0; k < LU; ++k)
-#pragma unroll
-        for (int e = 0; e < N; ++e)
-            d[k][e] = !colok[k] ? 0.0 : fused_pro ? ld_sc1(p.D + col[k] + e) : p.D[col[k] + e];
     int base = 0;   // stays a multiple of NB: ring slots are static
     // rows issued before tcache stream non-temporally, the rest allocate in the caches
     for (; base + NB + PF <= tcache; base += NB) {
@@ -664,7 +503,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
                 for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
     }
     if ((o.ls || o.rows_out) && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) {   // block-uniform
-        if (o.ls) op_linesearch(p, o.ngroups, o.fuse);
+        if (o.ls) op_linesearch(p, o.ngroups);
         else op_rows_scalars(p, o);
     }
 }
@@ -977,27 +816,6 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
             }
         }
     }
-}
-
-// The fused tail's slices as a launch of their own, on k_onepass's grid and block -> (row group,
-// segment) map, so every slice is computed by the same code in the same order as in the prologue
-// (bitwise the same iterates wherever a run of iterations is cut).  UPDATE (the flush: before an
-// exact-gradient refresh and at the end of every bpgl_solver_step): apply the pending update, if
-// any; the last block to arrive records it.  !UPDATE: the shrink alone (after a reset or refresh).
-template <bool UPDATE>
-__global__ __launch_bounds__(kThreads) void k_onepass_slices(Params p, OnePassArgs o, int BC) {
-    if (p.st->done) return;
-    const int b = blockIdx.x, SB = o.SB;
-    int grp, sb;
-    if (o.xl) { grp = (b & 7) + 8 * ((b >> 3) / SB); sb = (b >> 3) % SB; }
-    else { grp = b / SB; sb = b % SB; }
-    if (!UPDATE) {
-        op_slice<false, false>(p, o, grp, sb, BC, 0.0);
-        return;
-    }
-    if (op_tail_pending(p)) op_slice<true, false>(p, o, grp, sb, BC, p.st->gamma);
-    // k_onepass's grid size: the arrival counter stays a multiple of it after every launch
-    if (op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x) && threadIdx.x == 0) op_tail_applied(p.st);
 }
 
 }  // namespace bpgl
