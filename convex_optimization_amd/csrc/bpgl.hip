@@ -179,10 +179,12 @@ void geometry(bpgl_ctx* c) {
         c->op_ngroups = (int)ng;
         c->op_R = (int)R;
         c->op_xl = (ng % 8 == 0) ? 1 : 0;   // each row group's blocks on one XCD (blockIdx % 8)
-        // k_onepass_tail: 64-column tiles (one rank: one per block, its 4 waves split the row-group
-        // partials of U; row shards: U arrives summed, one tile per wave) and 256-row strides
-        c->op_tail_grid = c->rows ? (int)std::min<int64_t>(cdiv(c->wp, 64 * kWaves), kOpTailBlocks)
-                                  : (int)std::min<int64_t>(std::max(cdiv(c->m, kThreads), cdiv(c->wp, 64)), kOpTailBlocks);
+        // k_onepass_tail: 64-column tiles -- one per wave when U arrives summed (row shards) or each
+        // lane sums its column's few row-group partials (one rank, ngroups <= kOpTailWaveGroups); one per
+        // block otherwise, its 4 waves splitting the row groups -- and 256-row strides
+        c->op_tail_grid = c->rows || ng <= kOpTailWaveGroups
+                              ? (int)std::min<int64_t>(cdiv(c->wp, 64 * kWaves), kOpTailBlocks)
+                              : (int)std::min<int64_t>(std::max(cdiv(c->m, kThreads), cdiv(c->wp, 64)), kOpTailBlocks);
     } else {
         c->op_SB = c->op_ngroups = c->op_R = c->op_xl = c->op_tail_grid = 0;
     }
@@ -420,6 +422,8 @@ OnePassArgs op_tail_args(const bpgl_ctx* c) {
     } else if (c->op.fold) {   // one rank: k_onepass folded U already
         o.Us = c->op.Ufold;
         o.ngroups = 1;
+    } else {
+        o.tailw = c->op_ngroups <= kOpTailWaveGroups ? 1 : 0;
     }
     return o;
 }

@@ -54,6 +54,9 @@ constexpr int kOpMaxSB = 128;   // at most two granules per lane (GPL)
 constexpr unsigned kOpPolls = 1u << 16;
 constexpr int kOpTailBlocks = 1024;   // k_onepass_tail grid cap (= its shrink partial count)
 constexpr int kOpMaxGroups = 256;     // row groups (one block per CU: at most the CU count)
+// k_onepass_tail sums U per lane (one 64-column tile per wave) up to this many row groups; above it
+// (configs[3]: 256 groups of a 4096-column block) the 4 waves of a block split the groups of a tile
+constexpr int kOpTailWaveGroups = 32;
 
 struct OnePassArgs {
     double* G;                   // [wp]   gradient carried across iterations
@@ -68,6 +71,8 @@ struct OnePassArgs {
     long long fail_at;           // test hook: iteration whose launch reports a hand-off failure (-1: none)
     int rowb;                    // k_onepass_tail: blocks appended after the column blocks that only run
                                  // the residual update (0: the column blocks run it first, as before)
+    int tailw;                   // k_onepass_tail, one rank: every lane sums its column's U partials itself
+                                 // (wave-owned 64-column tiles, no LDS fold; ngroups <= kOpTailWaveGroups)
     // in-kernel fold of the U partials ("onepass_fold" = 1): the ngroups blocks of a column segment
     // meet at segcnt[sb] and each sums one slice of the segment's columns over the row groups
     int fold;                    // 1: fold inside k_onepass (no k_onepass_fold launch)
@@ -638,15 +643,41 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
     }
     const int cb0 = (int)gridDim.x - (UPDATE ? o.rowb : 0);   // column blocks
     const int lane0 = threadIdx.x & 63, wave0 = threadIdx.x >> 6;
-    // pre-summed U (row shards, or one rank after the in-kernel fold): each wave owns 64-column tiles
+    // pre-summed U (row shards, or one rank after the in-kernel fold), or (tailw) few row-group
+    // partials that each lane sums for its own column: each wave owns 64-column tiles
+    const bool wtile = o.ngroups == 1 || o.tailw;
     const long long tile0 = (long long)blockIdx.x * kWaves + wave0;
     const long long j0 = tile0 * 64 + lane0;
-    const bool pre = o.ngroups == 1 && (int)blockIdx.x < cb0 && j0 < p.wp;
+    const bool pre = wtile && (int)blockIdx.x < cb0 && j0 < p.wp;
+    // U of column j: the row groups summed in the order of the LDS fold below -- group q into
+    // accumulator q % 4 (increasing q), then ((a0 + a1) + a2) + a3 -- so both forms give the same bits
+    auto usum = [&](long long j) -> double {
+        if (!UPDATE) return 0.0;
+        if (o.Uf) return (double)o.Uf[j];
+        if (o.ngroups == 1) return o.Us[j];
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int q = 0;
+        for (; q + 16 <= o.ngroups; q += 16) {   // 16 loads in flight, then the adds in group order
+            double v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = o.Us[(long long)(q + k) * p.wp + j];
+#pragma unroll
+            for (int k = 0; k < 16; k += 4) { a0 += v[k]; a1 += v[k + 1]; a2 += v[k + 2]; a3 += v[k + 3]; }
+        }
+        for (; q < o.ngroups; ++q) {
+            const double v = o.Us[(long long)q * p.wp + j];
+            if ((q & 3) == 0) a0 += v;
+            else if ((q & 3) == 1) a1 += v;
+            else if ((q & 3) == 2) a2 += v;
+            else a3 += v;
+        }
+        return ((a0 + a1) + a2) + a3;
+    };
     double pg = 0.0, pu = 0.0, px = 0.0, pd = 0.0, pdg = 0.0, prc = 0.0;
     if (pre) {
         const bool col = j0 < p.w;
         pg = o.G[j0];
-        pu = !UPDATE ? 0.0 : o.Uf ? (double)o.Uf[j0] : o.Us[j0];
+        pu = usum(j0);
         px = col ? p.x[j0] : 0.0;
         pd = (UPDATE && col) ? p.D[j0] : 0.0;
         pdg = col ? p.diag[j0] : 0.0;
@@ -726,9 +757,9 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
         }
         p.D[j] = Dj;
     };
-    if (o.ngroups == 1) {
-        // U already summed (over ranks, or by k_onepass): every wave takes its own 64-column tiles;
-        // the first tile's operands were loaded at the head
+    if (wtile) {
+        // U already summed (over ranks, or by k_onepass) or summed per lane: every wave takes its own
+        // 64-column tiles; the first tile's operands were loaded at the head
         // (software-pipelined: the next tile's operands are loaded before this tile's shrink stores,
         // which the compiler could not move them past -- D and x are written in place)
         const long long tstep = (long long)cb * kWaves;
@@ -741,7 +772,7 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
             if (hn) {
                 const bool col = jn < p.w;
                 ng = o.G[jn];
-                nu = !UPDATE ? 0.0 : o.Uf ? (double)o.Uf[jn] : o.Us[jn];
+                nu = usum(jn);
                 nx = col ? p.x[jn] : 0.0;
                 nd = (UPDATE && col) ? p.D[jn] : 0.0;
                 ndg = col ? p.diag[jn] : 0.0;
