@@ -21,6 +21,7 @@ for rep in 1 2; do
     run $L $lib --config 3 --steps 64 --warmup 20 --ramp 64
     run $L $lib --m 1024 --steps 256 --warmup 200
     run $L $lib --m 2048 --steps 256 --warmup 200
+    run $L $lib --m 1024 --comm --shard rows --steps 256 --warmup 200
   done
 done
 cat $OUT
