@@ -866,55 +866,77 @@ def main():
             import gc as _gc
             _gc.collect()
             torch.cuda.empty_cache()
+
+        def leg(key, run):
+            # a side leg that raises (the same way on every rank: shapes and eligibility are
+            # rank-independent) is recorded, not fatal -- `value` above is already measured
+            try:
+                fresh()
+                run()
+            except Exception as e:
+                out[key] = {"error": f"{type(e).__name__}: {e}"[:400]}
+
         if not args.strong_total:
-            fresh()
-            res = measure(ctx, argparse.Namespace(**vars(args)), m, args.n_per_gpu)
-            out["strong"] = leg_summary(ctx, res, K, G, False)
-            out["strong"]["config"] = f"m={m} n={args.n_per_gpu} split {G} ways ({out['strong']['config']})"
+            def strong():
+                r2 = measure(ctx, argparse.Namespace(**vars(args)), m, args.n_per_gpu)
+                out["strong"] = leg_summary(ctx, r2, K, G, False)
+                out["strong"]["config"] = f"m={m} n={args.n_per_gpu} split {G} ways ({out['strong']['config']})"
+            leg("strong", strong)
         if args.block == 1 and rows and not args.exchange_fp32:
             # the same row split with the opt-in fp32 exchange (half the all-reduce bytes): with the
             # fp64 line, the strong leg and the column split, four message sizes per SCALE run for the
             # alpha / beta all-reduce model of DESIGN.md section 6.1
-            a2 = argparse.Namespace(**vars(args))
-            a2.exchange_fp32 = 1
-            fresh()
-            res = measure(ctx, a2, m, n_total)
-            out["rows_exchange_fp32"] = leg_summary(ctx, res, K, G, weak)
-            out["rows_exchange_fp32"]["config"] = (f"m={m} n={n_total} row-sharded, all-reduce of n+5 fp32 "
-                                                   f"({out['rows_exchange_fp32']['config']})")
+            def fp32_rows():
+                a2 = argparse.Namespace(**vars(args))
+                a2.exchange_fp32 = 1
+                r2 = measure(ctx, a2, m, n_total)
+                out["rows_exchange_fp32"] = leg_summary(ctx, r2, K, G, weak)
+                out["rows_exchange_fp32"]["config"] = (f"m={m} n={n_total} row-sharded, all-reduce of n+5 fp32 "
+                                                       f"({out['rows_exchange_fp32']['config']})")
+            leg("rows_exchange_fp32", fp32_rows)
         if args.block == 1 and rows:
             a2 = argparse.Namespace(**vars(args))
             a2.shard = "columns"
-            fresh()
-            res = measure(ctx, a2, m, n_total)
-            out["columns"] = leg_summary(ctx, res, K, G, weak)
-            out["columns"]["config"] = f"m={m} n={n_total} column-sharded ({out['columns']['config']})"
-            if not args.strong_total:
-                fresh()
-                res = measure(ctx, a2, m, args.n_per_gpu)
-                out["columns"]["strong"] = leg_summary(ctx, res, K, G, False)
+
+            def columns():
+                r2 = measure(ctx, a2, m, n_total)
+                out["columns"] = leg_summary(ctx, r2, K, G, weak)
+                out["columns"]["config"] = f"m={m} n={n_total} column-sharded ({out['columns']['config']})"
+            leg("columns", columns)
+            if not args.strong_total and "error" not in out["columns"]:
+                def columns_strong():
+                    r2 = measure(ctx, a2, m, args.n_per_gpu)
+                    out["columns"]["strong"] = leg_summary(ctx, r2, K, G, False)
+                try:
+                    fresh()
+                    columns_strong()
+                except Exception as e:
+                    out["columns"]["strong"] = {"error": f"{type(e).__name__}: {e}"[:400]}
         if not args.strong_total:
             fresh()
             ctx.barrier()
             n1 = None
             if ctx.rank == 0:
-                a3 = argparse.Namespace(**vars(args))
-                a3.comm = False
-                solo = SoloCtx(ctx)
-                res = measure(solo, a3, m, args.n_per_gpu)
-                n1 = window_rate(res, K)[0]
-                o = leg_summary(solo, res, K, 1, False)
+                try:   # rank 0 alone: it must reach the barrier below whatever happens
+                    a3 = argparse.Namespace(**vars(args))
+                    a3.comm = False
+                    solo = SoloCtx(ctx)
+                    res = measure(solo, a3, m, args.n_per_gpu)
+                    n1 = window_rate(res, K)[0]
+                    o = leg_summary(solo, res, K, 1, False)
+                except Exception as e:
+                    out["n1_same_run"] = {"error": f"{type(e).__name__}: {e}"[:400]}
             ctx.barrier()
-            if ctx.rank == 0:
+            if ctx.rank == 0 and n1:
                 o.update({"config": f"m={m} n={args.n_per_gpu} on rank 0's GPU alone (no communicator), same run",
                           "efficiency_weak_rows": out["value"] / (G * n1)})
-                if "strong" in out:
+                if "value" in out.get("strong", {}):
                     o["speedup_strong_rows"] = out["strong"]["value"] / n1
-                if "rows_exchange_fp32" in out:
+                if "value" in out.get("rows_exchange_fp32", {}):
                     o["efficiency_weak_rows_exchange_fp32"] = out["rows_exchange_fp32"]["value"] / (G * n1)
-                if "columns" in out:
+                if "value" in out.get("columns", {}):
                     o["efficiency_weak_columns"] = out["columns"]["value"] / (G * n1)
-                    if "strong" in out["columns"]:
+                    if "value" in out["columns"].get("strong", {}):
                         o["speedup_strong_columns"] = out["columns"]["strong"]["value"] / n1
                 out["n1_same_run"] = o
     if G == 1 and args.type == "float" and res is not None:
