@@ -119,8 +119,6 @@ def parse():
     ap.add_argument("--tail-row-blocks", type=int, default=-1, choices=[-1, 0, 1],
                     help="one-pass tail: residual update on blocks of its own (1, library default) or first in every block (0)")
     ap.add_argument("--onepass-variant", type=int, default=0, help="one-pass ring depth / prefetch variant (0-3)")
-    ap.add_argument("--onepass-wide", type=int, default=-1, choices=[-1, 0, 1],
-                    help="one-pass rows of 8 loads per lane (-1: auto, where 4 would need 2 granules per lane)")
     ap.add_argument("--onepass-fold", type=int, default=-1, choices=[-1, 0, 1],
                     help="one-pass U fold inside k_onepass (1) or in k_onepass_fold / the tail (0, library default)")
     ap.add_argument("--graph-max", type=int, default=-1,
@@ -248,7 +246,7 @@ class Ctx:
         return [float(t[0]) for t in out]
 
 
-def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, shard="rows", layout=None):
+def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, shard="rows"):
     import torch
     from convex_optimization_amd.distributed import RankComm, row_bounds, shard_bounds
     from convex_optimization_amd.parameters import device_instance
@@ -261,8 +259,7 @@ def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, sha
         idx = torch.cat([torch.arange(s, e) for s, e in bounds]).to(f"cuda:{ctx.local}")
         col_range = idx
     gc, b, mu, _ = device_instance(m, n_total, 0.4, block, TYPE=type_name, seed=seed, device=ctx.local,
-                                   comm=comm, col_range=col_range, row_range=row_range, cu_mask=ctx.cu_mask,
-                                   layout=layout)
+                                   comm=comm, col_range=col_range, row_range=row_range, cu_mask=ctx.cu_mask)
     torch.cuda.synchronize()
     return gc, b, mu
 
@@ -292,8 +289,7 @@ def measure(ctx, args, m, n_total):
     iterations; if a one-pass launch failed before the windows (every window then runs on the
     two-pass kernels), the solver is reset and the whole sequence measured once more."""
     import torch
-    layout = {"onepass_wide": args.onepass_wide} if getattr(args, "onepass_wide", -1) >= 0 else None
-    gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard, layout)
+    gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard)
     gc.set_tuning("fused", args.fused)
     gc.set_tuning("onepass", args.onepass)
     if args.exchange_fp32:

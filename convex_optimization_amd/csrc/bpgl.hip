@@ -123,12 +123,6 @@ struct bpgl_ctx {
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
     int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
-    // wide rows ("onepass_wide", before bpgl_bind; fp32 / fp64 A): 8 instead of 4 loads per lane and
-    // row (8192 fp32 columns per segment block) on a 7-row ring -- half the segment blocks per row, so
-    // half the per-row hand-off work per byte of A.  -1 (default): where 4 loads would need two
-    // granules per lane (SB > 64: the N = 8 row shard of configs[2]); 0 never; 1 whenever it fits
-    int op_wide_knob = -1;
-    bool op_wide = false;
     int op_rowb = 1;   // k_onepass_tail: residual update on blocks of its own ("tail_row_blocks" knob)
     // fold the U partials inside k_onepass ("onepass_fold" 1) or in k_onepass_fold / the tail (0, default:
     // the in-kernel form's write-through partials and segment barrier cost more than the launch it
@@ -174,12 +168,7 @@ void geometry(bpgl_ctx* c) {
     // one-pass geometry: SB segment blocks per row, floor(CUs / SB) row groups, one block per CU
     const int bc = c->dtype == BPGL_F32 ? OnePassGeo<4, float>::BC
                  : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<3, bf16_t>::BC;
-    int64_t SB = cdiv(c->wp, bc);
-    // wide rows: twice the columns per segment block, one granule per lane (SB <= 64) only
-    const int64_t SBw = cdiv(c->wp, 2 * (int64_t)bc);
-    c->op_wide = c->dtype != BPGL_BF16 && SBw <= 64 && SBw <= c->cus &&
-                 (c->op_wide_knob > 0 || (c->op_wide_knob < 0 && SB > 64));
-    if (c->op_wide) SB = SBw;
+    const int64_t SB = cdiv(c->wp, bc);
     c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
     c->op_gpl = SB > 64 ? 2 : 1;   // k_onepass<..., 2> relies on SB > 64
     if (c->op_shape) {
@@ -352,13 +341,6 @@ template <typename T> struct OpVar<T, 0> { static constexpr int NB = 16, PF = 3;
 template <typename T> struct OpVar<T, 1> { static constexpr int NB = 18, PF = 4; };
 template <typename T> struct OpVar<T, 2> { static constexpr int NB = 14, PF = 3; };
 template <typename T> struct OpVar<T, 3> { static constexpr int NB = 17, PF = 4; };
-// wide rows (LU 8, twice the bytes per row step): a ring of 5-7 rows, LAG 3-5 row steps (fp32:
-// 6 / 1 and 5 / 1 fit the 512 registers, 7 / 2 spills 60 bytes, 8 / 2 196)
-template <int V> struct OpVarW;
-template <> struct OpVarW<0> { static constexpr int NB = 6, PF = 1; };
-template <> struct OpVarW<1> { static constexpr int NB = 5, PF = 1; };
-template <> struct OpVarW<2> { static constexpr int NB = 7, PF = 1; };
-template <> struct OpVarW<3> { static constexpr int NB = 7, PF = 2; };
 template <> struct OpVar<bf16_t, 0> { static constexpr int NB = 12, PF = 2; };
 template <> struct OpVar<bf16_t, 1> { static constexpr int NB = 10, PF = 2; };
 template <> struct OpVar<bf16_t, 2> { static constexpr int NB = 11, PF = 2; };
@@ -377,8 +359,6 @@ Params op_params(const bpgl_ctx* c) {
 // GPL: granules per lane of the row hand-off (SB <= 64: 1, SB <= 128: 2)
 template <typename T, int V, int GPL>
 const void* onepass_fn_v() { return (const void*)k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU, GPL>; }
-template <typename T, int V>
-const void* onepass_fn_w() { return (const void*)k_onepass<T, OpVarW<V>::NB, OpVarW<V>::PF, 8, 1>; }
 template <typename T, int GPL>
 const void* onepass_fn_g(int v) {
     switch (v) {
@@ -389,21 +369,10 @@ const void* onepass_fn_g(int v) {
     }
 }
 template <typename T>
-const void* onepass_fn_wt(int v) {
-    switch (v) {
-        case 1: return onepass_fn_w<T, 1>();
-        case 2: return onepass_fn_w<T, 2>();
-        case 3: return onepass_fn_w<T, 3>();
-        default: return onepass_fn_w<T, 0>();
-    }
-}
-template <typename T>
 const void* onepass_fn_t(int v, int gpl) { return gpl == 2 ? onepass_fn_g<T, 2>(v) : onepass_fn_g<T, 1>(v); }
-const void* onepass_fn(const bpgl_ctx* c) {
-    const int v = c->op_variant, gpl = c->op_gpl;
-    if (c->op_wide) return c->dtype == BPGL_F32 ? onepass_fn_wt<float>(v) : onepass_fn_wt<double>(v);
-    return c->dtype == BPGL_F32 ? onepass_fn_t<float>(v, gpl)
-         : c->dtype == BPGL_F64 ? onepass_fn_t<double>(v, gpl) : onepass_fn_t<bf16_t>(v, gpl);
+const void* onepass_fn(int dtype, int v, int gpl) {
+    return dtype == BPGL_F32 ? onepass_fn_t<float>(v, gpl)
+         : dtype == BPGL_F64 ? onepass_fn_t<double>(v, gpl) : onepass_fn_t<bf16_t>(v, gpl);
 }
 template <typename T, int V, int GPL>
 void onepass_launch_v(bpgl_ctx* c) {
@@ -419,32 +388,12 @@ void onepass_launch_g(bpgl_ctx* c) {
         default: onepass_launch_v<T, 0, GPL>(c); break;
     }
 }
-template <typename T, int V>
-void onepass_launch_w(bpgl_ctx* c) {
-    hipLaunchKernelGGL((k_onepass<T, OpVarW<V>::NB, OpVarW<V>::PF, 8, 1>),
-                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, op_params(c), c->op);
-}
-template <typename T>
-void onepass_launch_wt(bpgl_ctx* c) {
-    switch (c->op_variant) {
-        case 1: onepass_launch_w<T, 1>(c); break;
-        case 2: onepass_launch_w<T, 2>(c); break;
-        case 3: onepass_launch_w<T, 3>(c); break;
-        default: onepass_launch_w<T, 0>(c); break;
-    }
-}
 template <typename T>
 void onepass_launch_t(bpgl_ctx* c) {
     if (c->op_gpl == 2) onepass_launch_g<T, 2>(c);
     else onepass_launch_g<T, 1>(c);
 }
 int onepass_launch(bpgl_ctx* c) {
-    if (c->op_wide) {
-        if (c->dtype == BPGL_F32) onepass_launch_wt<float>(c);
-        else onepass_launch_wt<double>(c);
-        LAUNCH_CHECK("k_onepass");
-        return 0;
-    }
     switch (c->dtype) {
         case BPGL_F32: onepass_launch_t<float>(c); break;
         case BPGL_F64: onepass_launch_t<double>(c); break;
@@ -523,7 +472,7 @@ const char* onepass_ineligible(bpgl_ctx* c) {
         return "column shards need a single rank without a communicator (row shards run it on several)";
     if (c->fused) return "not combined with the fused iteration";
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c), kThreads, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_variant, c->op_gpl), kThreads, 0) != hipSuccess || nb < 1)
         return "kernel does not fit on a CU";
     if ((int64_t)c->op_ngroups * c->op_SB > (int64_t)nb * c->cus) return "grid exceeds the resident capacity";
     return nullptr;
@@ -1299,8 +1248,6 @@ int bpgl_solver_stat(bpgl_ctx* c, const char* key, int64_t* value) {
     else if (!strcmp(key, "cus")) *value = c->cus;
     else if (!strcmp(key, "cu_masked")) *value = c->cu_masked ? 1 : 0;
     else if (!strcmp(key, "onepass_grid")) *value = (int64_t)c->op_ngroups * c->op_SB;
-    else if (!strcmp(key, "onepass_wide")) *value = c->op_wide ? 1 : 0;
-    else if (!strcmp(key, "onepass_sb")) *value = c->op_SB;
     else return fail(BPGL_E_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1404,13 +1351,6 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         if (c->bound) return fail(BPGL_E_STATE, "\"cus\" must be set before bpgl_bind (it sets the scratch layout)");
         if (value < 1 || value > c->dev_cus) return fail(BPGL_E_ARG, "cus must be in [1, %d]", c->dev_cus);
         c->cus = (int)value;
-        geometry(c);
-        return 0;
-    }
-    if (!strcmp(key, "onepass_wide")) {   // speed only (rounding-level: other s23 / U summation orders); sets the layout
-        if (c->bound) return fail(BPGL_E_STATE, "\"onepass_wide\" must be set before bpgl_bind (it sets the scratch layout)");
-        if (value < -1 || value > 1) return fail(BPGL_E_ARG, "onepass_wide must be -1, 0 or 1");
-        c->op_wide_knob = (int)value;
         geometry(c);
         return 0;
     }

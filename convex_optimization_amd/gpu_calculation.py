@@ -81,12 +81,10 @@ class GPU_Calculation:
     T_HEIGHT = 512
     TYPE = 'double'
 
-    def __init__(self, A, Block, device=None, comm=None, shard="columns", cu_mask=None, layout=None):
+    def __init__(self, A, Block, device=None, comm=None, shard="columns", cu_mask=None):
         """``cu_mask``: optional sequence of uint32 words (bit i = CU i) restricting the solver's
         stream to those CUs (several ranks sharing one GPU; see
-        ``distributed.xcd_symmetric_cu_mask``); the persistent one-pass grid is then sized to them.
-        ``layout``: optional {key: value} of the tuning knobs that must precede bpgl_bind because
-        they set the scratch layout (``onepass_wide``, ``cus``; include/bpgl.h bpgl_set_tuning)."""
+        ``distributed.xcd_symmetric_cu_mask``); the persistent one-pass grid is then sized to them."""
         if shard not in ("columns", "rows"):
             raise ValueError("shard must be 'columns' or 'rows'")
         self.shard = shard
@@ -96,7 +94,6 @@ class GPU_Calculation:
         self.device = _resolve_device(A, device)
         self._dt = N.dtype_code(self.TYPE)
         self._comm = comm
-        self._layout = dict(layout or {})
         self._ctx = None
         self.init_cpu_array(A)
         self.init_gpu_array(A)
@@ -128,8 +125,6 @@ class GPU_Calculation:
         assert L.bpgl_block_width_padded(ctx) == Wp
         if self.shard == "rows":
             N.check(L.bpgl_set_shard(ctx, N.BPGL_SHARD_ROWS), "bpgl_set_shard")
-        for key, value in self._layout.items():
-            N.check(L.bpgl_set_tuning(ctx, key.encode(), int(value)), "bpgl_set_tuning")
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             At = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))

@@ -53,7 +53,7 @@ def parameters(N, K, den, SAVE_FLAG=False, READ_FLAG=False, SILENCE=False, seed=
 
 
 def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal_cls=None, comm=None,
-                    col_range=None, row_range=None, cu_mask=None, layout=None):
+                    col_range=None, row_range=None, cu_mask=None):
     """Build (gpu_cal, b, mu, x_true) with A generated in HBM.
 
     A is drawn with torch's CUDA generator in fp32, its rows scaled to unit
@@ -63,7 +63,6 @@ def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal
     block; b is local, A^T b summed over ranks).  ``col_range``/``comm``: build only this rank's column shard (the
     full row normalisation is computed from row sums all ranks agree on).
     ``cu_mask``: passed to GPU_Calculation (the solver stream's CUs, several ranks on one GPU).
-    ``layout``: passed to GPU_Calculation (knobs that set the scratch layout, e.g. ``onepass_wide``).
     """
     import torch
     from .gpu_calculation import GPU_Calculation
@@ -97,7 +96,7 @@ def device_instance(N, K, den, Block, TYPE="float", seed=0, device=None, gpu_cal
     cls.TYPE = TYPE
     try:
         gc = cls(A, Block, device=dev, comm=comm, shard="rows" if row_range is not None else "columns",
-                 cu_mask=cu_mask, layout=layout)
+                 cu_mask=cu_mask)
     finally:
         cls.TYPE = old
     del A

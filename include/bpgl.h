@@ -206,8 +206,7 @@ double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
  *   enqueued), "fallbacks" (recoveries above), "requested"
  *   (iterations asked of bpgl_solver_step), "enqueued", "cus" (CUs the
  *   persistent grid is sized for), "cu_masked" (1: narrower than the device,
- *   from the stream's CU mask), "onepass_grid" (its blocks), "onepass_sb"
- *   (segment blocks per row), "onepass_wide" (1: rows of 8 loads per lane).
+ *   from the stream's CU mask), "onepass_grid" (its blocks).
  * bpgl_solver_residual: device pointer of the residual s11 = sum_k Ax_k - b (m).
  */
 int bpgl_solver_reset(bpgl_ctx* ctx, const double* b, double mu, double* x,
@@ -257,8 +256,7 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   "onepass" (default -1 = when eligible, 0 = off, 1 = required): one pass
  *   over A per iteration, the gradient carried as g += gamma A^T (A D); needs
  *   one feature block, one rank (or row shards), no fused mode, at most
- *   128 x 4096 columns (fp32; 128 x 6144 for bf16, 128 x 2048 for fp64; with
- *   onepass_wide up to 64 x 8192 fp32 / 64 x 4096 fp64) and all
+ *   128 x 4096 columns (fp32; 128 x 6144 for bf16, 128 x 2048 for fp64) and all
  *   of its blocks resident at once (nothing else running on the device).
  *   "onepass_cache_permille" (default -1 = auto: 750 when this rank's A block is
  *   at most 320 MiB, i.e. about the 256 MiB Infinity Cache, else 0): share of every
@@ -279,11 +277,6 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   "cus" (before bpgl_bind only; default: the stream's CU mask, else the device):
  *   the CU count the persistent one-pass grid (row groups x segment blocks) is
  *   sized for.
- *   "onepass_wide" (before bpgl_bind only; fp32 / fp64 A; default -1 = where
- *   4 loads per lane and row would need more than 64 segment blocks per row,
- *   0 = never, 1 = whenever at most 64 fit): rows of 8 loads per lane (8192 fp32
- *   columns per segment block) on a 5-8 row register ring -- half the segment
- *   blocks per row (one hand-off granule per lane), other summation order.
  * The environment variable BPGL_TARGET_BLOCKS (read by bpgl_create) sets the
  * number of (row chunk x column segment) tiles per two-pass launch (default
  * 1024 for fp32 A, 512 for fp64 / bf16). */

@@ -338,54 +338,3 @@ def test_in_kernel_fold_option(golden, use_graph):
     x1 = g2.run(b2, mu2, 120, use_graph=use_graph)["x"]
     assert g2.solver_stat("onepass") == 1 and g2.solver_stat("fallbacks") == 0
     assert rel(x1, x0) <= 1e-12, rel(x1, x0)
-
-
-# onepass_wide (include/bpgl.h): rows of 8 loads per lane, half the segment blocks per row; set
-# before bpgl_bind.  (m, n, dtype, knob, expected segment blocks per row)
-WIDE = [(1000, 4100, "float", 1, 1), (256, 262144, "float", 1, 32), (128, 300000, "float", -1, 37),
-        (128, 300000, "float", 0, 74), (2048, 8192, "double", 1, 2), (64, 2048 * 64, "double", 1, 32),
-        (300, 6000, "bf16", 1, 1)]
-
-
-@pytest.mark.parametrize("m,n,type_name,knob,sb", WIDE)
-def test_wide_rows(m, n, type_name, knob, sb):
-    """the wide geometry is chosen as documented (auto: where 4 loads per lane would need two hand-off
-    granules per lane; bf16 never) and reaches the two-pass iterates and the oracle as the default
-    geometry does (other summation order: rounding-level differences only); graph = eager bitwise"""
-    rs = np.random.RandomState(m + 3 * n)
-    A = rs.randn(m, n) / np.sqrt(n)
-    x_true = np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0)
-    b = A @ x_true + 0.01 * rs.randn(m)
-    mu = 0.1 * np.abs(A.T @ b).max()
-    gc = make_cls(type_name)(A, 1, device=0, layout={"onepass_wide": knob})
-    wide = 1 if (knob == 1 or (knob == -1 and sb * 2 > 64)) and type_name != "bf16" else 0
-    assert gc.solver_stat("onepass_wide") == wide and gc.solver_stat("onepass_sb") == sb
-    with pytest.raises(RuntimeError):   # the layout is fixed once bound
-        gc.set_tuning("onepass_wide", 1 - wide)
-    assert used_onepass(gc, b, mu)
-    one, two = both(gc, b, mu, 5)
-    assert rel(one["x"], two["x"]) <= 1e-12, rel(one["x"], two["x"])
-    one, two = both(gc, b, mu, 25)
-    assert rel(one["x"], two["x"]) <= 1e-8, rel(one["x"], two["x"])
-    assert one["t_last"] == two["t_last"]
-    np.testing.assert_array_equal(gc.run(b, mu, 40, use_graph=True)["x"],
-                                  gc.run(b, mu, 40, use_graph=False)["x"])
-    if m * n <= 40_000_000:
-        Ah = gc.A_b_gpu[0, :, :n].to(torch.float64).cpu().numpy()
-        ref = oracle.run(np.ascontiguousarray(Ah), b, mu, 1, 25)
-        assert rel(one["x"], ref["x"]) <= 1e-8, rel(one["x"], ref["x"])
-
-
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
-def test_wide_rows_reference_fixture(golden, variant):
-    """every wide ring variant on the reference's own fixture (<= 1e-9, as every solver test); the
-    variants differ only in ring depth and prefetch distance, so their iterates are bitwise equal"""
-    fx = golden("c1_b1_p1_f32in")
-    A = oracle.fixture_A(fx)
-    gc = make_cls("float")(A, 1, device=0, layout={"onepass_wide": 1})
-    gc.set_tuning("onepass_variant", variant)
-    gc.set_tuning("onepass", 1)
-    res = gc.run(fx["b"], float(fx["mu"]), int(fx["ITER_MAX"]))
-    assert rel(res["x"], fx["x"]) <= 1e-9
-    gc.set_tuning("onepass_variant", 0)
-    np.testing.assert_array_equal(res["x"], gc.run(fx["b"], float(fx["mu"]), int(fx["ITER_MAX"]))["x"])
