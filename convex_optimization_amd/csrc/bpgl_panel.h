@@ -105,8 +105,9 @@ struct PanelParams {
 constexpr int kLspRows = 1024;    // rows per line-search partial
 
 // Diagnostic builds only (tools/panel_diag.sh; never the shipped library): bit 0 drops the
-// A-side LDS-DMA pieces after the prologue, bit 1 the RHS-side ones -- wrong results, used
-// to split a pass's time into MFMA + LDS and each stream's share.
+// A-side LDS-DMA pieces after the prologue, bit 1 the RHS-side ones, bits 2 / 3 half / all of the
+// lo operand pieces (panel_op_piece) -- wrong results, used to split a pass's time into MFMA + LDS
+// and each stream's share.
 #ifndef BPGL_PANEL_DIAG
 #define BPGL_PANEL_DIAG 0
 #endif
@@ -177,6 +178,10 @@ __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__
     const int rr = pc * 8 + (lane >> 3);
     const int c = swz128(rr, lane & 7);
     const int hl = rr / G::K, rhs = rr % G::K;
+    // diagnostic builds: bit 2 drops every other lo piece (3/4 of the operand bytes), bit 3 every lo
+    // piece (the hi bytes alone) -- the MFMA work unchanged, results wrong
+    if ((BPGL_PANEL_DIAG & 4) && NS == 2 && pc * 8 >= G::K && (pc & 1)) return;
+    if ((BPGL_PANEL_DIAG & 8) && NS == 2 && pc * 8 >= G::K) return;
     glds16o((hl ? lo : hi) + (long long)rhs * ld + ks + 8 * c, obuf + pc * 1024);
 }
 // pass-1 A stage: rows ks..ks+63 of A, columns col0..col0+255 -> [64][512 B] (a piece = 2 rows)

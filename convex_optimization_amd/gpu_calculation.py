@@ -20,7 +20,7 @@ semantics (gpu_calculation.py:141-292) so the reference drivers
     crosses PCIe.
 
 New: ``run`` -- the whole solver loop resident on the
-device, captured once as hipGraphs of 1 and 8 iterations, returning x, which
+device, captured once as hipGraphs of 1, 2, 4, ..., 64 iterations, returning x, which
 the reference's drivers never did (lasso.py:167-169, :609).  With one feature
 block an iteration is ``k_onepass`` (A read once: s23 = A D and U = A^T s23,
 the line search by its last row group) + ``k_onepass_tail`` (x, Ax, r,

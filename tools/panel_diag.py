@@ -13,7 +13,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     lib, k = sys.argv[1], int(sys.argv[2])
-    ilv = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    ilv = int(sys.argv[3]) if len(sys.argv) > 3 else 1   # -1: the library's per-pass defaults
     import torch
     from convex_optimization_amd import _native
     _native.LIB_PATH = os.path.abspath(lib)
@@ -23,7 +23,8 @@ def main():
     A = torch.randn(m, n, device="cuda", generator=g)
     pl = PanelLasso(A, 1, nrhs=k, device=0)
     del A
-    pl.set_tuning("interleave", ilv)
+    if ilv >= 0:
+        pl.set_tuning("interleave", ilv)
     B = torch.randn(m, k, device="cuda", generator=g, dtype=torch.float64)
     pl.solver_reset(B, 0.1, use_graph=False)
     pl.set_kernel_timing(True)
