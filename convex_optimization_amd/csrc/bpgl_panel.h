@@ -106,13 +106,17 @@ constexpr int kLspRows = 1024;    // rows per line-search partial
 
 // Diagnostic builds only (tools/panel_diag.sh; never the shipped library): bit 0 drops the
 // A-side LDS-DMA pieces after the prologue, bit 1 the RHS-side ones, bits 2 / 3 half / all of the
-// lo operand pieces (panel_op_piece) -- wrong results, used to split a pass's time into MFMA + LDS
-// and each stream's share.
+// lo operand pieces (panel_op_piece), bit 4 the lo MFMAs -- wrong results, used to split a pass's
+// time into MFMA + LDS and each stream's share.
 #ifndef BPGL_PANEL_DIAG
 #define BPGL_PANEL_DIAG 0
 #endif
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
+// diagnostic bit 4: the lo MFMAs are not issued (their fragments are still read) -- the share of a
+// pass that the lo product's matrix-core work costs
+constexpr bool kPanelDiagNoLoMfma = (BPGL_PANEL_DIAG & 16) != 0;
+__device__ __forceinline__ void panel_keep(const bf16x8& v) { asm volatile("" ::"v"(v)); }
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -318,9 +322,10 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 #pragma unroll
                 for (int mt = 0; mt < 4; ++mt) {
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    if constexpr (NS == 2)
+                    if constexpr (NS == 2 && !kPanelDiagNoLoMfma)
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
                 }
+                if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(b_lo);
                 if constexpr (ILV) {
                     if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
                     __builtin_amdgcn_sched_group_barrier(0x8, 4 * NS, 0);
@@ -423,9 +428,10 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][0], acc[mt][nt], 0, 0, 0);
-                if constexpr (NS == 2)
+                if constexpr (NS == 2 && !kPanelDiagNoLoMfma)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][1], acc[mt][nt], 0, 0, 0);
             }
+            if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(bfr[cb][1]);
         });
         abuf = abuf_next;
     }
@@ -526,9 +532,10 @@ __device__ __forceinline__ void panel_mainloop_stag(char* smem, const __bf16* __
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     acc[mt][2 * q + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bhi[j], acc[mt][2 * q + j], 0, 0, 0);
-                    if constexpr (NS == 2)
+                    if constexpr (NS == 2 && !kPanelDiagNoLoMfma)
                         acc[mt][2 * q + j] =
                             __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], blo[j], acc[mt][2 * q + j], 0, 0, 0);
+                    if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(blo[j]);
                 }
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);

@@ -27,6 +27,10 @@ def main():
         pl.set_tuning("interleave", ilv)
     B = torch.randn(m, k, device="cuda", generator=g, dtype=torch.float64)
     pl.solver_reset(B, 0.1, use_graph=False)
+    warm = int(os.environ.get("PANEL_DIAG_WARMUP", "0"))   # untimed iterations first (clock ramp)
+    if warm:
+        pl.solver_step(warm)
+        pl.stream.synchronize()
     pl.set_kernel_timing(True)
     pl.solver_step(30)
     pl.stream.synchronize()
