@@ -106,8 +106,8 @@ constexpr int kLspRows = 1024;    // rows per line-search partial
 
 // Diagnostic builds only (tools/panel_diag.sh; never the shipped library): bit 0 drops the
 // A-side LDS-DMA pieces after the prologue, bit 1 the RHS-side ones, bits 2 / 3 half / all of the
-// lo operand pieces (panel_op_piece), bit 4 the lo MFMAs -- wrong results, used to split a pass's
-// time into MFMA + LDS and each stream's share.
+// lo operand pieces (panel_op_piece), bit 4 the lo MFMAs, bit 5 the lo MFMAs at twice the rate -- wrong
+// results, used to split a pass's time into MFMA + LDS and each stream's share.
 #ifndef BPGL_PANEL_DIAG
 #define BPGL_PANEL_DIAG 0
 #endif
@@ -117,6 +117,19 @@ typedef __attribute__((address_space(3))) void* lds_void_ptr;
 // pass that the lo product's matrix-core work costs
 constexpr bool kPanelDiagNoLoMfma = (BPGL_PANEL_DIAG & 16) != 0;
 __device__ __forceinline__ void panel_keep(const bf16x8& v) { asm volatile("" ::"v"(v)); }
+// diagnostic bit 5: the lo product's MFMAs replaced by block-scaled e4m3 ones at twice the bf16 rate
+// (v_mfma_scale_f32_32x32x64_f8f6f4, 4 per wave and stage = half the lo matrix cycles) on the raw bits
+// of the fragments, into accumulators of their own -- the time and clock a 2x-rate lo product would
+// run at, before any conversion cost (results wrong)
+constexpr bool kPanelDiagF8Lo = (BPGL_PANEL_DIAG & 32) != 0;
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ i32x8 panel_pack8(const bf16x8& x, const bf16x8& y) {
+    i32x8 r;
+    __builtin_memcpy(&r, &x, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&r) + 16, &y, 16);
+    return r;
+}
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -256,6 +269,11 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 #pragma unroll
         for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    f32x16 accd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) accd[i][e] = 0.f;
     // piece i of stage (so, sa): i < LO -> k-wide piece, else A piece i - LO (this order is what
     // the counted wait below assumes: the youngest LA operations are A pieces)
     auto piece = [&](int i, int so, int bo, int sa, int ba) {
@@ -322,10 +340,16 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 #pragma unroll
                 for (int mt = 0; mt < 4; ++mt) {
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    if constexpr (NS == 2 && !kPanelDiagNoLoMfma)
+                    if constexpr (NS == 2 && !kPanelDiagNoLoMfma && !kPanelDiagF8Lo)
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
                 }
                 if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(b_lo);
+                if constexpr (NS == 2 && kPanelDiagF8Lo && nt % 2 == 0) {
+                    constexpr int i = h * 2 + nt / 2;
+                    accd[i] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                        panel_pack8(af[(i & 1) * 2], af[(i & 1) * 2 + 1]), panel_pack8(b_hi, b_lo), accd[i], 0, 0, 0, 127, 0,
+                        127);
+                }
                 if constexpr (ILV) {
                     if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
                     __builtin_amdgcn_sched_group_barrier(0x8, 4 * NS, 0);
@@ -334,6 +358,9 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
         });
         abuf = abuf == 2 ? 0 : abuf + 1;
     }
+    if constexpr (kPanelDiagF8Lo)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[0][0][0] += accd[i][0] * 0.0f;
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
@@ -389,6 +416,11 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
         if constexpr (NS == 2) blo = panel_bfrag(ob, G::K + rhs, h, lane);
     };
 
+    f32x16 accd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) accd[i][e] = 0.f;
     // prologue: op(0), A(0), A(1), then stage 0 landed and group 0's fragments read
     for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
     for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
@@ -428,13 +460,22 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][0], acc[mt][nt], 0, 0, 0);
-                if constexpr (NS == 2 && !kPanelDiagNoLoMfma)
+                if constexpr (NS == 2 && !kPanelDiagNoLoMfma && !kPanelDiagF8Lo)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][1], acc[mt][nt], 0, 0, 0);
             }
             if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(bfr[cb][1]);
+            if constexpr (NS == 2 && kPanelDiagF8Lo && nt % 2 == 0) {
+                constexpr int i = h * 2 + nt / 2;
+                accd[i] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                    panel_pack8(af[ca][(i & 1) * 2], af[ca][(i & 1) * 2 + 1]), panel_pack8(bfr[cb][0], bfr[cb][1]),
+                    accd[i], 0, 0, 0, 127, 0, 127);
+            }
         });
         abuf = abuf_next;
     }
+    if constexpr (kPanelDiagF8Lo)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[0][0][0] += accd[i][0] * 0.0f;
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
