@@ -106,8 +106,8 @@ constexpr int kLspRows = 1024;    // rows per line-search partial
 
 // Diagnostic builds only (tools/panel_diag.sh; never the shipped library): bit 0 drops the
 // A-side LDS-DMA pieces after the prologue, bit 1 the RHS-side ones, bits 2 / 3 half / all of the
-// lo operand pieces (panel_op_piece), bit 4 the lo MFMAs, bit 5 the lo MFMAs at twice the rate -- wrong
-// results, used to split a pass's time into MFMA + LDS and each stream's share.
+// lo operand pieces (panel_op_piece), bit 4 the lo MFMAs, bit 5 the lo MFMAs at twice the rate, bit 6 all
+// MFMAs as 32x32x16 -- wrong results, used to split a pass's time into MFMA + LDS and each stream's share.
 #ifndef BPGL_PANEL_DIAG
 #define BPGL_PANEL_DIAG 0
 #endif
@@ -122,6 +122,10 @@ __device__ __forceinline__ void panel_keep(const bf16x8& v) { asm volatile("" ::
 // of the fragments, into accumulators of their own -- the time and clock a 2x-rate lo product would
 // run at, before any conversion cost (results wrong)
 constexpr bool kPanelDiagF8Lo = (BPGL_PANEL_DIAG & 32) != 0;
+// diagnostic bit 6: every hi and lo 16x16x32 MFMA group replaced by the same MACs on 32x32x16 bf16
+// MFMAs (half the operand-register reads per MAC) into accumulators of their own (results wrong) --
+// whether the 32 x 32 shape's lower energy per MAC raises the clock a power-limited pass holds
+constexpr bool kPanelDiag32 = (BPGL_PANEL_DIAG & 64) != 0;
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ i32x8 panel_pack8(const bf16x8& x, const bf16x8& y) {
@@ -338,7 +342,7 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
                 bf16x8 b_lo;
                 if constexpr (NS == 2) b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
 #pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
+                for (int mt = 0; mt < 4 && !kPanelDiag32; ++mt) {
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
                     if constexpr (NS == 2 && !kPanelDiagNoLoMfma && !kPanelDiagF8Lo)
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
@@ -350,6 +354,13 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
                         panel_pack8(af[(i & 1) * 2], af[(i & 1) * 2 + 1]), panel_pack8(b_hi, b_lo), accd[i], 0, 0, 0, 127, 0,
                         127);
                 }
+                if constexpr (NS == 2 && kPanelDiag32) {
+                    constexpr int t = (nt >> 1) * 2;
+                    accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b_hi, accd[t], 0, 0, 0);
+                    accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], b_hi, accd[t + 1], 0, 0, 0);
+                    accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b_lo, accd[t], 0, 0, 0);
+                    accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[3], b_lo, accd[t + 1], 0, 0, 0);
+                }
                 if constexpr (ILV) {
                     if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
                     __builtin_amdgcn_sched_group_barrier(0x8, 4 * NS, 0);
@@ -358,7 +369,7 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
         });
         abuf = abuf == 2 ? 0 : abuf + 1;
     }
-    if constexpr (kPanelDiagF8Lo)
+    if constexpr (kPanelDiagF8Lo || kPanelDiag32)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[0][0][0] += accd[i][0] * 0.0f;
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
@@ -458,7 +469,7 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
                 read_b(obn, 0, 0, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
             }
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
+            for (int mt = 0; mt < 4 && !kPanelDiag32; ++mt) {
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][0], acc[mt][nt], 0, 0, 0);
                 if constexpr (NS == 2 && !kPanelDiagNoLoMfma && !kPanelDiagF8Lo)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][1], acc[mt][nt], 0, 0, 0);
@@ -470,10 +481,17 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
                     panel_pack8(af[ca][(i & 1) * 2], af[ca][(i & 1) * 2 + 1]), panel_pack8(bfr[cb][0], bfr[cb][1]),
                     accd[i], 0, 0, 0, 127, 0, 127);
             }
+            if constexpr (NS == 2 && kPanelDiag32) {
+                constexpr int t = (nt >> 1) * 2;
+                accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][0], bfr[cb][0], accd[t], 0, 0, 0);
+                accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][2], bfr[cb][0], accd[t + 1], 0, 0, 0);
+                accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][1], bfr[cb][1], accd[t], 0, 0, 0);
+                accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][3], bfr[cb][1], accd[t + 1], 0, 0, 0);
+            }
         });
         abuf = abuf_next;
     }
-    if constexpr (kPanelDiagF8Lo)
+    if constexpr (kPanelDiagF8Lo || kPanelDiag32)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[0][0][0] += accd[i][0] * 0.0f;
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
