@@ -11,8 +11,9 @@ into the rate at its amortised cost, below); with several feature blocks, or
 across column shards, it is the reference's two passes (A^T r, then A D).
 
   N = 1 : BASELINE configs[1]  m=8192 n=65536 fp32 A, one feature block.
-  N > 1 : BASELINE configs[2]  m=8192 n=65536*N (n = 524288 at N = 8), weak scaling:
-          every GPU holds 2 GiB of A, the per-GPU work of N = 1.  The split
+  N > 1 : the metric's own unit on the metric's own matrix: iterations/s of the fixed
+          8192 x 65536 fp32 problem split N ways (strong scaling, "scaling": "strong";
+          speedup_vs_n1 = value / the N = 1 rate measured in the same run).  The split
           (--shard auto) follows the cost model of DESIGN.md section 6: one feature
           block -> rows (GPU g holds rows [g m/N, (g+1) m/N) of A, all columns,
           streams them once per iteration with k_onepass, and ONE RCCL all-reduce of
@@ -20,14 +21,14 @@ across column shards, it is the reference's two passes (A^T r, then A D).
           products and the failure flag); several feature blocks -> columns (the
           reference's P-way split, cpu_calculation.py:23-27: two passes over A per
           iteration and one all-reduce of m + 2 + N fp64 on the residual side).
-          The work unit is one "block-iteration" = one iteration's worth of an
-          8192 x 65536 fp32 matrix (the whole configs[1] matrix), so value = N x
-          global iterations/s.  Beside it, from the same run: "strong" (the fixed
-          8192 x 65536 matrix split N ways by rows), "columns" (the reference's
-          column split of the same weak problem, and its strong form), each with
-          its per-rank all-reduce times, and "n1_same_run" (rank 0 alone on the
-          N = 1 problem, with the efficiencies of the legs against it) and
-          "rows_exchange_fp32" (the row split with the opt-in fp32 exchange).
+          Beside it, from the same run: "weak" (BASELINE configs[2]'s shape,
+          m=8192 n=65536*N -- n = 524288 at N = 8 -- every GPU holding the 2 GiB of
+          N = 1; unit block-iters/s = N x global iterations/s, with its own
+          speedup_vs_n1), "columns" (the reference's column split of the same
+          problem, and its weak form), each with its per-rank all-reduce times,
+          "n1_same_run" (rank 0 alone on the N = 1 problem) and "rows_exchange_fp32"
+          (the row split with the opt-in fp32 exchange).  --weak makes the weak
+          problem the value line (the rounds 1-3 form).
   --config 2: configs[2]'s own problem (m=8192 n=524288) split over the N GPUs
           (strong scaling; at N = 1 the whole 16 GiB matrix on one GPU).
   --config 3 / 4: configs[3] (1048576 x 4096 fp32) / configs[4] (k = 128
@@ -109,7 +110,10 @@ def parse():
     ap.add_argument("--n-per-gpu", type=int, default=N_PER_GPU)
     ap.add_argument("--block", type=int, default=1)
     ap.add_argument("--type", default="float", choices=["float", "double", "bf16"])
-    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling leg (N > 1)")
+    ap.add_argument("--no-strong", action="store_true", help="skip the side legs of an N > 1 run")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: value = weak scaling (m=8192, n=65536 N, block-iters/s) instead of the default "
+                         "strong scaling of the metric's 8192 x 65536 matrix")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=20190325)
@@ -176,6 +180,19 @@ def parse():
     return a
 
 
+def main_shape(args, G):
+    """(n_total, scaling) of the value line: N = 1 -> the configured matrix ("none"); N > 1 -> the
+    metric's named 8192 x 65536 matrix split N ways ("strong"), configs[2]'s own matrix split N ways
+    with --config 2 ("strong"), or the weak problem m x 65536 N with --weak ("weak")"""
+    if G == 1:
+        return args.n_per_gpu, "none"
+    if args.strong_total:
+        return args.n_per_gpu * G, "strong"
+    if args.weak:
+        return args.n_per_gpu * G, "weak"
+    return args.n_per_gpu, "strong"
+
+
 def workload_label(args, G, m, n_total, ml, w, rows):
     """configs[K] label from the actual shape (BASELINE.json configs)."""
     if args.config == 2 or (m, n_total) == (8192, 524288):
@@ -184,6 +201,8 @@ def workload_label(args, G, m, n_total, ml, w, rows):
         name = "configs[3]"
     elif (m, n_total) == (8192, 65536) and G == 1:
         name = "configs[1]"
+    elif (m, n_total) == (8192, 65536):
+        name = f"configs[1] matrix (the metric's 8192x65536) split {G} ways, strong scaling"
     elif m == 8192 and n_total == 65536 * G:
         name = "configs[2]-style weak scaling"
     else:
@@ -276,6 +295,11 @@ def timed_window(ctx, sync, step, steps):
     return ctx.max(t1 - t0)
 
 
+class MeasureError(RuntimeError):
+    """every timed window of a measurement was invalid (an Exception, so a side leg records it and
+    every rank still reaches the closing barrier and rank 0 prints the line)"""
+
+
 def median(v):
     v = sorted(v)
     k = len(v)
@@ -344,8 +368,8 @@ def measure(ctx, args, m, n_total):
         if any(w["valid"] for w in wins) and eager_op == op0:
             break
         if attempt == 1:
-            raise SystemExit("every timed window lost one-pass iterations or fell back to two passes "
-                             "(another process holds CUs?)")
+            raise MeasureError("every timed window lost one-pass iterations or fell back to two passes "
+                               "(another process holds CUs?)")
     assert st["iters"] == args.warmup + n_ev + args.windows * args.steps or st["stopped"], st
     return dict(gc=gc, windows=wins, el_events=el_ev, n_events=n_ev, kernel_ms=times, samples=samples, status=st,
                 refresh_ms=refresh_ms, refresh_period=period, w_local=gc.MAT_WIDTH, m_local=gc.MAT_HEIGHT,
@@ -381,6 +405,7 @@ def leg_summary(ctx, res, K, G, weak):
     kms = res["kernel_ms"]
     return {"value": v * G if weak else v,
             "unit": "block-iters/s" if weak else "iters/s",
+            "scaling": ("weak" if weak else "strong") if G > 1 else "none",
             "ms_per_step": 1e3 / v,
             "ms_per_step_raw_median": raw * 1e3,
             "config": f"{res['m_local']} rows x {res['w_local']} cols per GPU",
@@ -669,7 +694,7 @@ def main_panel(args):
         "metric": METRIC.replace("fp32", "bf16") + f", {k} right-hand sides",
         "value": iters_s, "unit": f"iters/s ({k} right-hand sides per iteration)",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": el_graph / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": el_graph / args.steps * 1e3, "higher_is_better": True, "scaling": "none",
         "vs_baseline": None,
         "dtype": "bf16 (A) x hi+lo bf16 residual x " + ("hi+lo bf16" if d_split == 2 else "bf16") +
                  " direction, fp32 MFMA accumulate, fp64 reduce",
@@ -751,7 +776,7 @@ def main():
     ctx = Ctx(args.gpus)
     G = ctx.world
     m = args.m
-    n_total = args.n_per_gpu * G
+    n_total, scaling = main_shape(args, G)
     res = measure(ctx, args, m, n_total)
     w, ml = res["w_local"], res["m_local"]
     rows = res["gc"].shard == "rows"
@@ -777,7 +802,7 @@ def main():
     achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
     workload_key = f"m{m}_n{n_total}_b{args.block}_{args.type}_g{G}" + ("_rows" if rows and G > 1 else "")
     traffic = pmc_traffic(workload_key, kname)
-    weak = G > 1 and not args.strong_total
+    weak = scaling == "weak"
     ms_step = el_med / K * 1e3
     allreduce_ms = ctx.gather(kms.get("allreduce", 0.0)) if G > 1 or args.comm else None
     out = {
@@ -790,9 +815,10 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "strong" if args.strong_total and G > 1 else "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
+        "a_dtype": {"float": "fp32", "double": "fp64", "bf16": "bf16"}[args.type],
         "data": "synthetic (A ~ N(0,1) rows unit-norm, generated in HBM; x_true density 0.4; b = A x_true + 0.01 e)",
         "config": {
             "workload": workload_label(args, G, m, n_total, ml, w, rows),
@@ -856,10 +882,11 @@ def main():
     out["config"]["measure_attempts"] = res["attempts"]
     out["config"]["cus_per_rank"] = res["cus"]
     if G > 1 and not args.no_strong:
-        # the other legs of one SCALE run: the same fixed matrix split N
-        # ways (strong), the reference's column split (two passes, all-reduce of m + 2 + N on the
-        # residual side, cpu_calculation.py:23-27) beside the row split, and rank 0 alone on the
-        # N = 1 problem -- so the split choice and both efficiencies come from one run
+        # the other legs of one SCALE run: the other scaling form (weak:
+        # configs[2]'s shape, or strong when --weak made the weak problem the value line), the
+        # reference's column split (two passes, all-reduce of m + 2 + N on the residual side,
+        # cpu_calculation.py:23-27) beside the row split, and rank 0 alone on the N = 1 problem --
+        # so the split choice and both speedups come from one run
         def fresh():   # drop the previous leg's context, A and communicator before the next
             nonlocal res
             res = None
@@ -867,24 +894,30 @@ def main():
             _gc.collect()
             torch.cuda.empty_cache()
 
-        def leg(key, run):
+        def leg(key, run, into=None):
             # a side leg that raises (the same way on every rank: shapes and eligibility are
-            # rank-independent) is recorded, not fatal -- `value` above is already measured
+            # rank-independent; MeasureError is an Exception) is recorded, not fatal -- `value`
+            # above is already measured
             try:
                 fresh()
                 run()
             except Exception as e:
-                out[key] = {"error": f"{type(e).__name__}: {e}"[:400]}
+                (out if into is None else into)[key] = {"error": f"{type(e).__name__}: {e}"[:400]}
 
+        other = None   # the other scaling form of the default problem: (key, n_total, weak)
         if not args.strong_total:
-            def strong():
-                r2 = measure(ctx, argparse.Namespace(**vars(args)), m, args.n_per_gpu)
-                out["strong"] = leg_summary(ctx, r2, K, G, False)
-                out["strong"]["config"] = f"m={m} n={args.n_per_gpu} split {G} ways ({out['strong']['config']})"
-            leg("strong", strong)
+            other = ("strong", args.n_per_gpu, False) if weak else ("weak", args.n_per_gpu * G, True)
+
+            def other_leg():
+                r2 = measure(ctx, argparse.Namespace(**vars(args)), m, other[1])
+                o = leg_summary(ctx, r2, K, G, other[2])
+                o["config"] = (f"m={m} n={other[1]} " + ("(configs[2] shape at N = 8), " if other[2] else "") +
+                               f"split {G} ways ({o['config']})")
+                out[other[0]] = o
+            leg(other[0], other_leg)
         if args.block == 1 and rows and not args.exchange_fp32:
             # the same row split with the opt-in fp32 exchange (half the all-reduce bytes): with the
-            # fp64 line, the strong leg and the column split, four message sizes per SCALE run for the
+            # fp64 line, the other leg and the column split, four message sizes per SCALE run for the
             # alpha / beta all-reduce model of DESIGN.md section 6.1
             def fp32_rows():
                 a2 = argparse.Namespace(**vars(args))
@@ -903,15 +936,11 @@ def main():
                 out["columns"] = leg_summary(ctx, r2, K, G, weak)
                 out["columns"]["config"] = f"m={m} n={n_total} column-sharded ({out['columns']['config']})"
             leg("columns", columns)
-            if not args.strong_total and "error" not in out["columns"]:
-                def columns_strong():
-                    r2 = measure(ctx, a2, m, args.n_per_gpu)
-                    out["columns"]["strong"] = leg_summary(ctx, r2, K, G, False)
-                try:
-                    fresh()
-                    columns_strong()
-                except Exception as e:
-                    out["columns"]["strong"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+            if other is not None and "error" not in out["columns"]:
+                def columns_other():
+                    r2 = measure(ctx, a2, m, other[1])
+                    out["columns"][other[0]] = leg_summary(ctx, r2, K, G, other[2])
+                leg(other[0], columns_other, into=out["columns"])
         if not args.strong_total:
             fresh()
             ctx.barrier()
@@ -924,21 +953,13 @@ def main():
                     res = measure(solo, a3, m, args.n_per_gpu)
                     n1 = window_rate(res, K)[0]
                     o = leg_summary(solo, res, K, 1, False)
-                except Exception as e:
+                except BaseException as e:   # noqa: B036 -- never skip the barrier
                     out["n1_same_run"] = {"error": f"{type(e).__name__}: {e}"[:400]}
             ctx.barrier()
             if ctx.rank == 0 and n1:
-                o.update({"config": f"m={m} n={args.n_per_gpu} on rank 0's GPU alone (no communicator), same run",
-                          "efficiency_weak_rows": out["value"] / (G * n1)})
-                if "value" in out.get("strong", {}):
-                    o["speedup_strong_rows"] = out["strong"]["value"] / n1
-                if "value" in out.get("rows_exchange_fp32", {}):
-                    o["efficiency_weak_rows_exchange_fp32"] = out["rows_exchange_fp32"]["value"] / (G * n1)
-                if "value" in out.get("columns", {}):
-                    o["efficiency_weak_columns"] = out["columns"]["value"] / (G * n1)
-                    if "value" in out["columns"].get("strong", {}):
-                        o["speedup_strong_columns"] = out["columns"]["strong"]["value"] / n1
+                o["config"] = f"m={m} n={args.n_per_gpu} on rank 0's GPU alone (no communicator), same run"
                 out["n1_same_run"] = o
+                speedups(out, n1, G)
     if G == 1 and args.type == "float" and res is not None:
         out["config"]["vendor_gemv_yardstick"] = vendor_yardstick(res["gc"])
         out["config"]["vendor_iteration_yardstick"] = vendor_iteration_yardstick(res["gc"], res["b"], res["mu"])
@@ -946,6 +967,25 @@ def main():
         emit(out)
     if ctx.world > 1:
         ctx.dist.destroy_process_group()
+
+
+def speedups(out, n1, G):
+    """speedup_vs_n1 of the value line and of every leg against the N = 1 rate of the same run: a
+    strong line's iters/s / n1, a weak line's block-iters/s / n1 (= N x its efficiency); the weak
+    forms also carry efficiency = speedup / N"""
+    def put(o):
+        if isinstance(o, dict) and "value" in o:
+            o["speedup_vs_n1"] = o["value"] / n1
+            if o.get("scaling") == "weak" or str(o.get("unit", "")).startswith("block"):
+                o["efficiency_vs_n1"] = o["value"] / (G * n1)
+    put(out)
+    for key in ("strong", "weak", "rows_exchange_fp32"):
+        put(out.get(key))
+    col = out.get("columns")
+    put(col)
+    if isinstance(col, dict):
+        for key in ("strong", "weak"):
+            put(col.get(key))
 
 
 def parse_shard_auto():

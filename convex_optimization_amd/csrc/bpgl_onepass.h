@@ -227,6 +227,10 @@ __device__ bool op_fold_segment(const Params& p, const OnePassArgs& o, int grp, 
     if (threadIdx.x == 0) {
         unsigned long long* c = o.segcnt + sb;
         const unsigned long long ng = (unsigned long long)o.ngroups;
+        // release / acquire at agent scope around the meeting: the partials are written and read
+        // through sc1 (write-through / L2-bypassing) already, the fences make the ordering explicit
+        // across XCDs instead of resting on that cache policy
+        __atomic_thread_fence(__ATOMIC_RELEASE);   // agent scope: the HIP default for device code
         const unsigned long long old = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long target = (old / ng + 1) * ng;
         unsigned n = kOpPolls;
@@ -235,6 +239,7 @@ __device__ bool op_fold_segment(const Params& p, const OnePassArgs& o, int grp, 
             if (n-- == 0) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(2);
         }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
         seg_ok = ok;
     }
     __syncthreads();

@@ -77,26 +77,34 @@ def shard_rows(A, rank, nranks):
 
 
 def xcd_symmetric_cu_mask(rank, nranks, cus=256):
-    """CU mask words (bit i = CU i) giving rank `rank` of `nranks` (1, 2 or 4) processes that share
-    one GPU a disjoint 1/nranks of its CUs, the same number on every XCD.
+    """CU mask words (bit i = CU i) giving rank `rank` of `nranks` (1, 2, 4 or 8) processes that
+    share one GPU a disjoint 1/nranks of its CUs, the same number on every XCD.
 
-    The mask is built so that it does not depend on how the driver maps mask bits to XCDs: every
-    32-bit word is split into four bytes and a rank takes whole bytes (rank k of 2: bytes k and
-    k + 2; of 4: byte k).  A byte holds 8 consecutive bits, one of each residue mod 8 (bits
-    interleaved over the 8 XCDs) and a word is one XCD's 32 CUs (bits in XCD-sized runs), so
-    either way every XCD gets 32/nranks of the rank's CUs.  The one-pass grid is persistent: an XCD
-    left without CUs would never run its share of blocks."""
-    if nranks not in (1, 2, 4):
-        raise ValueError("CU partitions are built for 1, 2 or 4 ranks per GPU")
+    The mask is built so that it does not depend on how the driver maps mask bits to XCDs: bits
+    interleaved over the 8 XCDs (bit i on XCD i mod 8) or in XCD-sized runs (word j = XCD j's 32
+    CUs).  For 1, 2 or 4 ranks every 32-bit word is split into four bytes and a rank takes whole
+    bytes (rank k of 2: bytes k and k + 2; of 4: byte k): a byte holds one bit of each residue
+    mod 8 and a word is one XCD, so either way every XCD gets 32/nranks of the rank's CUs.  For 8
+    ranks (4 CUs per XCD each; needs 8 words) rank k takes, in word j, the four bits of residue
+    (k + j) mod 8: 4 bits of every word (runs), and over the 8 words 4 bits of every residue
+    (interleaved).  The one-pass grid is persistent: an XCD left without CUs would never run its
+    share of blocks."""
+    if nranks not in (1, 2, 4, 8):
+        raise ValueError("CU partitions are built for 1, 2, 4 or 8 ranks per GPU")
     if not 0 <= rank < nranks:
         raise ValueError(f"rank {rank} out of range for {nranks}")
     if cus % 32:
         raise ValueError("the device's CU count must be a multiple of 32")
+    words = cus // 32
+    if nranks == 8:
+        if words != 8:
+            raise ValueError("8 CU partitions need 8 XCD-sized mask words (256 CUs)")
+        return [sum(1 << (8 * q + (rank + j) % 8) for q in range(4)) for j in range(words)]
     per = 4 // nranks
     word = 0
     for k in range(per):
         word |= 0xFF << (8 * (rank + k * nranks))
-    return [word] * (cus // 32)
+    return [word] * words
 
 
 def row_exchange_layout(wp):

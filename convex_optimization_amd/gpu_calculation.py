@@ -302,11 +302,19 @@ class GPU_Calculation:
         N.check(N.lib().bpgl_solver_stat(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_solver_stat")
         return v.value
 
-    def solver_x(self):
-        """Current iterate as a host ndarray (K_local,) in the reference's block order.  Goes
-        through solver_status first, so iterations a failed one-pass launch lost are re-run
-        before x is read (RCCL row shards: every rank must call it, as solver_status)."""
-        self.solver_status()
+    def solver_x(self, complete=True):
+        """Current iterate as a host ndarray (K_local,) in the reference's block order.
+
+        complete=True (default) goes through solver_status first, so iterations a failed one-pass
+        launch lost are re-run before x is read.  That call is COLLECTIVE for RCCL row shards (a
+        pending recovery enqueues all-reduces): every rank must call it, as solver_status.  A caller
+        that reads x on some ranks only (a gather on rank 0, say) passes complete=False on those
+        ranks after a collective solver_status() -- x is then read as it stands, with no
+        communication."""
+        if complete:
+            self.solver_status()
+        else:
+            self.stream.synchronize()
         return self._x[:, :self.MAT_WIDTH].reshape(-1).cpu().numpy().copy()
 
     def _ctx_residual(self):
@@ -319,9 +327,13 @@ class GPU_Calculation:
         """Device view of x; call solver_status() first (it re-runs lost one-pass iterations)."""
         return self._x[:, :self.MAT_WIDTH]
 
-    def solver_records(self):
-        """(err_iter, time_iter) host copies, after solver_status (as solver_x)."""
-        self.solver_status()
+    def solver_records(self, complete=True):
+        """(err_iter, time_iter) host copies, after solver_status (as solver_x; collective for RCCL
+        row shards unless complete=False)."""
+        if complete:
+            self.solver_status()
+        else:
+            self.stream.synchronize()
         if self._err_iter is None:
             return None, None
         return self._err_iter.cpu().numpy().copy(), self._time_iter.cpu().numpy().copy()

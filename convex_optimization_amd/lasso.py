@@ -196,18 +196,20 @@ class ClassLassoDevice(_Driver):
                     break
         else:
             gc.solver_step(self.ITER_MAX)
+        # solver_status is collective for RCCL row shards (a pending one-pass recovery enqueues
+        # all-reduces): every rank runs this driver; the reads after it need no communication
         st = gc.solver_status()
         wall = time.time() - start
         t = st["t_last"]
         if record:
-            e, ti = gc.solver_records()
+            e, ti = gc.solver_records(complete=False)
             if rec_err:
                 err_iter[:] = e[:len(err_iter)]
             if rec_time:
                 time_iter[:] = ti[:len(time_iter)]
         t_elapsed = time_iter[t] if rec_time else wall
         self.rlt_display(SILENCE, t_elapsed, t)
-        self.x = gc.solver_x().reshape(-1, 1)
+        self.x = gc.solver_x(complete=False).reshape(-1, 1)
         self.iters = st["iters"]
         self.stopped = st["stopped"]
         return t_elapsed

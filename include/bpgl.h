@@ -53,7 +53,12 @@ typedef struct bpgl_ctx bpgl_ctx;
 /* Message of the last failing call on this thread ("" if none). */
 const char* bpgl_last_error(void);
 
-/* Library / ABI version (major * 10000 + minor * 100 + patch). */
+/* Library / ABI version (major * 10000 + minor * 100 + patch).
+ *   100 (0.1.0): the first ABI.
+ *   200 (0.2.0): + bpgl_stream_create / bpgl_stream_destroy; bpgl_iterate always synchronises
+ *                the solver stream before returning; the "onepass_cache_permille" default moved
+ *                from 0 to -1 (automatic: 750 when the rank's A block fits the Infinity Cache);
+ *                panel tuning key "lo8" (e4m3 lo products) and "r_refresh". */
 int bpgl_version(void);
 
 /*

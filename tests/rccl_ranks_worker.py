@@ -67,8 +67,10 @@ def main():
     out = {"cus": np.int64(gc.solver_stat("cus")), "cu_masked": np.int64(gc.solver_stat("cu_masked")),
            "onepass_grid": np.int64(gc.solver_stat("onepass_grid"))}
     for graph in (True, False):
-        if graph and rank == a.fail_rank and a.fail_at >= 0:   # the first (graph) solve only
-            gc.set_tuning("onepass_fail_at", a.fail_at)
+        if rank == a.fail_rank and a.fail_at >= 0:
+            # the first (graph) solve only; cleared explicitly before the eager solve rather than
+            # relying on the library's one-shot hook (round 3: the hook once fired in both solves)
+            gc.set_tuning("onepass_fail_at", a.fail_at if graph else -1)
         # every rank's set-up is finished before any rank's solve starts (nothing else on the GPU)
         torch.cuda.synchronize()
         dist.barrier()

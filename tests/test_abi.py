@@ -14,7 +14,7 @@ from convex_optimization_amd import panel  # noqa: F401  (registers the bpgl_pan
 
 def test_library_present_and_loads():
     assert os.path.exists(N.LIB_PATH), "run __graft_entry__.build() first"
-    assert N.lib().bpgl_version() >= 100
+    assert N.lib().bpgl_version() >= 200
 
 
 def test_every_header_symbol_exported():

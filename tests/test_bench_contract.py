@@ -178,3 +178,47 @@ def test_multi_gpu_legs_carry_both_splits():
     assert strong["value"] == v and strong["unit"] == "iters/s"
     solo = b.SoloCtx(type("C", (), {"local": 3})())
     assert (solo.rank, solo.world, solo.local) == (0, 1, 3) and solo.max(2.0) == 2.0 and solo.gather(1) == [1.0]
+
+
+def test_multi_gpu_value_is_the_metric_unit():
+    """N > 1: value is iterations/s of the metric's named 8192 x 65536 fp32 matrix split N ways
+    (strong scaling); the weak problem (n = 65536 N, block-iters/s) is the side leg "weak", and
+    --weak / --config 2 keep their own shapes; N = 1 reports "scaling": "none\""""
+    b = _bench()
+    for G in (2, 4, 8):
+        a = _parse(b, ["--gpus", str(G)])
+        assert (a.m, b.main_shape(a, G)) == (8192, (65536, "strong"))
+        a = _parse(b, ["--gpus", str(G), "--weak"])
+        assert b.main_shape(a, G) == (65536 * G, "weak")
+    a = _parse(b, [])
+    assert b.main_shape(a, 1) == (65536, "none")
+    import os as _os
+    _os.environ["WORLD_SIZE"] = "8"
+    try:
+        a = _parse(b, ["--config", "2", "--gpus", "8"])
+    finally:
+        del _os.environ["WORLD_SIZE"]
+    assert b.main_shape(a, 8) == (524288, "strong")
+    assert b.workload_label(_parse(b, []), 8, 8192, 65536, 1024, 65536, True).startswith(
+        "configs[1] matrix (the metric's 8192x65536) split 8 ways")
+
+
+def test_speedups_against_the_same_run_n1():
+    """speedup_vs_n1 on the value line and every leg; efficiency only on the weak forms"""
+    b = _bench()
+    out = {"value": 1000.0, "scaling": "strong",
+           "weak": {"value": 6000.0, "unit": "block-iters/s", "scaling": "weak"},
+           "columns": {"value": 400.0, "unit": "iters/s", "scaling": "strong",
+                       "weak": {"value": 2000.0, "unit": "block-iters/s", "scaling": "weak"}},
+           "rows_exchange_fp32": {"error": "x"}}
+    b.speedups(out, 250.0, 8)
+    assert out["speedup_vs_n1"] == 4.0 and "efficiency_vs_n1" not in out
+    assert out["weak"]["speedup_vs_n1"] == 24.0 and out["weak"]["efficiency_vs_n1"] == 3.0
+    assert out["columns"]["speedup_vs_n1"] == 1.6 and out["columns"]["weak"]["speedup_vs_n1"] == 8.0
+    assert "speedup_vs_n1" not in out["rows_exchange_fp32"]
+
+
+def test_measure_error_is_an_exception():
+    """a side leg whose windows are all invalid must be recorded, not end the run"""
+    b = _bench()
+    assert issubclass(b.MeasureError, Exception)

@@ -222,7 +222,7 @@ def test_xcd_symmetric_cu_masks():
     import pytest
     from convex_optimization_amd.distributed import xcd_symmetric_cu_mask
     cus = 256
-    for nranks in (1, 2, 4):
+    for nranks in (1, 2, 4, 8):
         masks = [xcd_symmetric_cu_mask(r, nranks, cus) for r in range(nranks)]
         bits = [{i for i in range(cus) if (m[i // 32] >> (i % 32)) & 1} for m in masks]
         assert set().union(*bits) == set(range(cus))
@@ -231,6 +231,8 @@ def test_xcd_symmetric_cu_masks():
             assert [sum(1 for i in b if i % 8 == x) for x in range(8)] == [32 // nranks] * 8
             assert [sum(1 for i in b if i // 32 == x) for x in range(8)] == [32 // nranks] * 8
     with pytest.raises(ValueError):
-        xcd_symmetric_cu_mask(0, 8)
+        xcd_symmetric_cu_mask(0, 3)
+    with pytest.raises(ValueError):
+        xcd_symmetric_cu_mask(0, 8, 128)
     with pytest.raises(ValueError):
         xcd_symmetric_cu_mask(2, 2)

@@ -8,7 +8,7 @@ multi-rank cases sum the exchange buffers in the test, here the product's ncclAl
 the captured graph and eager) is the exchange.  Row shards on a shared GPU cannot keep the
 one-pass kernel's blocks co-resident unless every rank's stream is confined to its own CUs:
 without CU masks they normally finish on the two-pass row iteration (DESIGN.md section 6.2);
-with XCD-symmetric CU masks (``--cumask``: 2 ranks x 128 CUs, 4 ranks x 64 CUs) each rank's
+with XCD-symmetric CU masks (``--cumask``: 2 ranks x 128 CUs, 4 x 64, 8 x 32) each rank's
 persistent grid is sized to its CUs and the default N > 1 path -- one-pass row shards, k_onepass
 + k_onepass_fold + ncclAllReduce of [U | r.s23 | s23.s23 | failed] + k_onepass_tail -- runs
 end to end with no fallback.  Tolerance: the reference fixture's x within 1e-9 relative l2
@@ -52,7 +52,8 @@ def rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
 
 
-@pytest.mark.parametrize("case,world", [("c1_b2_p4_f32in", 2), ("bound_b4_p2_f32in", 2), ("c1_b2_p4_f32in", 4)])
+@pytest.mark.parametrize("case,world", [("c1_b2_p4_f32in", 2), ("bound_b4_p2_f32in", 2), ("c1_b2_p4_f32in", 4),
+                                        ("c1_b2_p4_f32in", 8)])
 def test_two_rccl_ranks_column_shards(golden, case, world, tmp_path):
     from convex_optimization_amd import distributed as D
     fx = golden(case)
@@ -85,7 +86,7 @@ def test_two_rccl_ranks_row_shards(golden, world, tmp_path):
     print("row-shard fallbacks per rank:", [int(o["fallbacks"]) for o in out])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_row_shards_onepass_cu_masked(golden, world, tmp_path):
     """The default N > 1 iteration (one-pass row shards over RCCL), every rank on its own CUs:
     no rank falls back, x is bit-identical on every rank and matches the reference fixture

@@ -1,7 +1,7 @@
 // Where do the blocks of a kernel launched on a CU-masked stream run?  
 //
-// For each of the masks distributed.xcd_symmetric_cu_mask builds (1, 2 and 4 partitions of the
-// 256 CUs) this launches a grid of short spinning blocks on a stream created with
+// For each of the masks distributed.xcd_symmetric_cu_mask builds (1, 2, 4 and 8 partitions
+// of the 256 CUs) this launches a grid of short spinning blocks on a stream created with
 // hipExtStreamCreateWithCUMask and records, per block, the XCC id and the HW_ID register
 // (SE / SH / CU of the block), then prints the number of distinct CUs each XCD ran blocks on.
 // A mask that left an XCD without CUs would leave that XCD's blocks undispatched, so the masks
@@ -45,11 +45,18 @@ int main() {
     CHECK(hipMalloc(&d, 8 * G));
     std::vector<unsigned> h(2 * G);
     printf("device CUs %d\n", cus);
-    for (int nranks : {1, 2, 4}) {
+    for (int nranks : {1, 2, 4, 8}) {
         for (int rank = 0; rank < nranks; ++rank) {
             unsigned word = 0;
-            for (int k = 0; k < 4 / nranks; ++k) word |= 0xFFu << (8 * (rank + k * nranks));
-            std::vector<uint32_t> mask(words, word);
+            std::vector<uint32_t> mask(words, 0u);
+            if (nranks == 8) {   // word j: the four bits of residue (rank + j) mod 8
+                for (int j = 0; j < words; ++j)
+                    for (int q = 0; q < 4; ++q) mask[j] |= 1u << (8 * q + (rank + j) % 8);
+                word = mask[0];
+            } else {
+                for (int k = 0; k < 4 / nranks; ++k) word |= 0xFFu << (8 * (rank + k * nranks));
+                for (auto& v : mask) v = word;
+            }
             hipStream_t s;
             CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask.data()));
             uint32_t back[32] = {};
@@ -70,7 +77,7 @@ int main() {
             }
             int xcc_of_b[8] = {};
             for (int b = 0; b < 8; ++b) xcc_of_b[b] = (int)h[2 * b];
-            printf("partitions %d rank %d mask word 0x%08x (stream reports %d CUs):", nranks, rank, word, nb);
+            printf("partitions %d rank %d mask word[0] 0x%08x (stream reports %d CUs):", nranks, rank, word, nb);
             for (int x = 0; x < 8; ++x) printf(" xcd%d=%zu", x, per[x].size());
             printf("  blocks 0-7 on xcd");
             for (int b = 0; b < 8; ++b) printf(" %d", xcc_of_b[b]);
