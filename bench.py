@@ -158,6 +158,12 @@ def parse():
     ap.add_argument("--op-pad", type=int, default=0,
                     help="panel path: bf16 elements appended to each RHS row of the operand images (multiple of 64)")
     ap.add_argument("--lda-pad", type=int, default=0, help="panel path: columns appended to each row of bf16 A")
+    ap.add_argument("--lo8", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
+                    help="panel path: e4m3 lo products, bit 0 pass 1 (residual), bit 1 pass 2 (direction); "
+                         "-1: library default")
+    ap.add_argument("--r-refresh", type=int, default=-1,
+                    help="panel path with lo8 in pass 2: exact residual refresh period (multiple of 8; 0 never; "
+                         "-1: library default)")
     ap.add_argument("--defer-x", type=int, default=-1, choices=[-1, 0, 1],
                     help="panel path, one block: apply x += gamma D in the next pass-1 epilogue (1) or in the "
                          "update kernel (0); -1: library default")
@@ -652,6 +658,10 @@ def main_panel(args):
         pl.set_tuning("defer_x", args.defer_x)
     if args.write_through >= 0:
         pl.set_tuning("write_through", args.write_through)
+    if args.lo8 >= 0:
+        pl.set_tuning("lo8", args.lo8)
+    if args.r_refresh >= 0:
+        pl.set_tuning("r_refresh", args.r_refresh)
     for q in (1, 2):
         if getattr(args, f"waves{q}") >= 0:
             pl.set_tuning(f"waves{q}", getattr(args, f"waves{q}"))
@@ -705,6 +715,7 @@ def main_panel(args):
             "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
             "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
             "defer_x": pl.get_tuning("defer_x"), "op_pad": pl.get_tuning("op_pad"), "lda_pad": args.lda_pad,
+            "lo8": pl.get_tuning("lo8"), "r_refresh": pl.get_tuning("r_refresh"), "refreshes": pl.stat("refreshes"),
             "interleave12": [pl.get_tuning("interleave1"), pl.get_tuning("interleave2")],
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,

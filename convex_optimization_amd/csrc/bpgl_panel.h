@@ -100,6 +100,10 @@ struct PanelParams {
     PanelState* st;
     unsigned long long* cnt;   // [k] k_panel_reduce arrivals per RHS (monotone: launch q ends at q * groups)
     int wt;             // write-through store sites: 1 pass-1 epilogue (x, D'), 2 pass-2 slab, 4 S, 8 R
+    // e4m3 lo products (the "lo8" knob, section "lo8" below)
+    unsigned* amax;     // float bits of max |A| (k_panel_diag)
+    int* rexp;          // [k][m / 256]   frexp exponent of max |R| per 256-row group (update, reset, refresh)
+    int* dexp;          // [w / 256][k]   frexp exponent of max |D| per 256-column tile (pass-1 epilogue)
 };
 
 constexpr int kLspRows = 1024;    // rows per line-search partial
@@ -607,6 +611,180 @@ __device__ __forceinline__ void panel_mainloop_stag(char* smem, const __bf16* __
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
+// ---------------------------------------------------------------------------
+// lo8: the lo product on block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, twice the bf16
+// rate).  A k = 128 pass is power-limited: the same ~470k cycles with or without the lo MFMAs, but
+// the bf16 lo product's matrix-core energy pulls the clock from ~2.4 to ~1.9 GHz.
+// Here acc += A (hi) in bf16 as before and acc += A8 (lo8) once per 128 K, where
+//   A8  = e4m3(A / 2^sa): one scale for all of A, max |A| < 2^(sa + 8) (k_panel_diag's max);
+//   lo8 = e4m3(lo / 2^s): per lane (its RHS), |lo| <= 2^(e - 9) for max |v| < 2^e, s = e - 17,
+// so both images stay within +-256 (e4m3fn: +-448); the MFMA's E8M0 scales (127 + sa, 127 + s)
+// undo the division exactly.  The images come from the same bf16 fragments the hi MFMAs read:
+// v_mfma_scale_f32_16x16x128_f8f6f4 pairs byte i of lane l's A operand (row l & 15, K-group l >> 4)
+// with byte i of lane l's B operand (column l & 15, K-group l >> 4) and writes C in the common
+// 16 x 16 layout (tools/mfma_f8_probe.hip, profiles/r03/mfma_f8_probe), so the four 8-value
+// fragments a lane holds for K-half h of stages 2t and 2t + 1 -- byte 8 (2 par + h) + i = element i
+// of the fragment, the same K on both sides -- form one operand, with no lane movement.  Operand
+// precision: e4m3 keeps 4 significant bits, so the lo term carries ~2^-4 of its 2^-9: ~2^-13
+// relative to the product (hi + lo bf16: ~2^-17; d_split = 1: 2^-9).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// 8 bf16 -> 8 e4m3 bytes of v / scale (round to nearest even) into dwords 2 SLOT (values 0-3) and
+// 2 SLOT + 1 (values 4-7) of an MFMA operand
+template <int SLOT>
+__device__ __forceinline__ void panel_fp8x8(const bf16x8& v, float scale, i32x8& dst) {
+    s16x2 a = {0, 0}, b = {0, 0};
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(a, bf16x2{v[0], v[1]}, scale, false);
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(a, bf16x2{v[2], v[3]}, scale, true);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(b, bf16x2{v[4], v[5]}, scale, false);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(b, bf16x2{v[6], v[7]}, scale, true);
+    dst[2 * SLOT] = __builtin_bit_cast(int, a);
+    dst[2 * SLOT + 1] = __builtin_bit_cast(int, b);
+}
+constexpr int kExpZero = -1000;   // exponent recorded for an all-zero group
+__device__ __forceinline__ int panel_frexp(double v) {
+    int e = kExpZero;
+    if (v > 0.0) (void)frexp(v, &e);
+    return e;
+}
+__device__ __forceinline__ int panel_clamp_exp(int s) { return s < -126 ? -126 : (s > 126 ? 126 : s); }
+// scale exponent of a lo piece whose hi + lo values stay below 2^e: |lo| / 2^(e - 17) <= 256
+__device__ __forceinline__ int panel_lo_exp(int e) { return panel_clamp_exp(e - 17); }
+// scale exponent of A's e4m3 image from the max |A| recorded by k_panel_diag: |A| / 2^sa < 256
+__device__ __forceinline__ int panel_a_exp(const unsigned* amax) {
+    int e = 0;
+    (void)frexpf(__uint_as_float(*amax), &e);
+    return panel_clamp_exp(e - 8);
+}
+
+// The ILV 0 / 1 mainloop (panel_mainloop) with the lo product on e4m3, stages taken in pairs
+// (nsteps must be even: the host requires 128 | the pass's K range).  esrc: this pass's exponent
+// table, lane RHS r over ent entries at esrc[r * erstride + t * etstride]; the lane scale is the
+// max over them.  a_exp: A's scale exponent.
+template <int NT, int PASS, int ILV, int WNX>
+__device__ __forceinline__ void panel_mainloop_lo8(char* smem, const __bf16* __restrict__ A, long long lda,
+                                                   long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
+                                                   const __bf16* __restrict__ bl, long long ldb, long long b_k0,
+                                                   int nsteps, const int* __restrict__ esrc, long long erstride,
+                                                   long long etstride, int ent, int a_exp,
+                                                   f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
+    using G = PanelGeo<NT, 2, WNX>;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    char* abufs = smem;
+    char* obufs = smem + kPanelNA * kPanelAStage;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // lane scales: lane l reduces the exponents of RHS wn * RW + l % RW (RW = this wave's RHS), then
+    // N-tile nt takes lane nt * 16 + (l & 15)'s result.  All loads are issued before the reduction.
+    constexpr int RW = G::NTW * 16;
+    int emax = kExpZero;
+    {
+        const int* er = esrc + (long long)(wn * RW + lane % RW) * erstride;
+        for (int t0 = 0; t0 < ent; t0 += 32) {
+            int ev[32];
+#pragma unroll
+            for (int t = 0; t < 32; ++t) ev[t] = t0 + t < ent ? er[(long long)(t0 + t) * etstride] : kExpZero;
+#pragma unroll
+            for (int t = 0; t < 32; ++t) emax = ev[t] > emax ? ev[t] : emax;
+        }
+    }
+    float b_sc[G::NTW];
+    int b_e8[G::NTW];
+#pragma unroll
+    for (int nt = 0; nt < G::NTW; ++nt) {
+        const int sb = panel_lo_exp(__shfl(emax, nt * 16 + (lane & 15)));
+        b_sc[nt] = ldexpf(1.0f, sb);
+        b_e8[nt] = 127 + sb;
+    }
+    const float a_sc = ldexpf(1.0f, a_exp);
+    const int a_e8 = 127 + a_exp;
+
+    auto piece = [&](int i, int so, int bo, int sa, int ba) {
+        if (i < G::LO) {
+            panel_op_piece<NT, 2, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
+                                       lane);
+        } else if (PASS == 1) {
+            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+                                    abufs + ba * kPanelAStage, wave, lane);
+        } else {
+            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+                                    abufs + ba * kPanelAStage, wave, lane);
+        }
+    };
+    constexpr int NP = G::LO + G::LA;
+    constexpr int NG = 2 * G::NTW;
+    constexpr int PPG = (NP + NG - 1) / NG;
+    // prologue: op(0), A(0), A(1) -- the loop's counted wait assumes exactly this issue order
+#pragma unroll
+    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
+#pragma unroll
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
+#pragma unroll
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
+    i32x8 a8[4], b8[G::NTW];
+    int abuf = 0;
+    auto stage = [&](int s, auto parc) {
+        constexpr int par = decltype(parc)::value;
+        wait_vm_barrier<G::LA>();
+        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
+        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
+        if (!ILV) {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) piece(i, so, bo, sa, ba);
+        }
+        const char* ab = abufs + abuf * kPanelAStage;
+        const char* ob = obufs + (s & 1) * G::OStage;
+        static_for<0, 2>([&](auto hc) {
+            constexpr int h = decltype(hc)::value;
+            constexpr int slot = 2 * par + h;
+            bf16x8 af[4];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+                af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
+                                   : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) panel_fp8x8<slot>(af[mt], a_sc, a8[mt]);
+            static_for<0, G::NTW>([&](auto ntc) {
+                constexpr int nt = decltype(ntc)::value;
+                constexpr int grp = h * G::NTW + nt;
+                constexpr int p0 = grp * PPG < NP ? grp * PPG : NP;
+                constexpr int p1 = (grp + 1) * PPG < NP ? (grp + 1) * PPG : NP;
+                if constexpr (ILV) {
+                    static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
+                }
+                const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
+                const bf16x8 b_hi = panel_bfrag(ob, rhs, h, lane);
+                const bf16x8 b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
+                panel_fp8x8<slot>(b_lo, b_sc[nt], b8[nt]);
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
+                if constexpr (par == 1 && h == 1) {
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                            a8[mt], b8[nt], acc[mt][nt], 0, 0, 0, a_e8, 0, b_e8[nt]);
+                }
+                if constexpr (ILV) {
+                    if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x8, (par == 1 && h == 1) ? 8 : 4, 0);
+                }
+            });
+        });
+        abuf = abuf == 2 ? 0 : abuf + 1;
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+        stage(s, std::integral_constant<int, 0>{});
+        stage(s + 1, std::integral_constant<int, 1>{});
+    }
+    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
+}
+
 // Write-through (sc1) stores for the bulk outputs a kernel hands to the next launch (split-K
 // slab, D', x, S, R and its split): the lines do not sit dirty in the XCD L2s at the kernel
 // boundary, whose cost grows by ~1 us per 6 MB left dirty (MI355X_MICROARCH.md, "boundary").
@@ -673,7 +851,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             }
         return;
     }
-    double* nred = reinterpret_cast<double*>(smem);   // [4 wm][k][3]
+    double* nred = reinterpret_cast<double*>(smem);   // [4 wm][k][4]
     // one feature block: the previous iteration's x += gamma D' (k_panel_update leaves it
     // pending) is applied here, from the D' this thread is about to overwrite -- the same
     // arithmetic as k_panel_update's x part, so x is bitwise unchanged by the deferral
@@ -684,7 +862,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
         const double mu = p.mu[rhs];
         const double gprev = fx ? p.gamma[rhs] : 0.0;
-        double sbx = 0.0, sx = 0.0, err = 0.0;
+        double sbx = 0.0, sx = 0.0, err = 0.0, dmax = 0.0;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
             const long long j = c0 + wm * 64 + mt * 16 + (lane >> 4) * 4;   // 4 consecutive columns
@@ -712,6 +890,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 const long long kx = (long long)mb * p.w + j + r;
                 const double bx = p.rec[kx] * soft_thr(p.diag[kx] * x - g, mu);
                 double dprime;
+                dmax = fmax(dmax, fabs(bx - x));
                 if constexpr (DS == 2) {
                     split_bf16(bx - x, dh[r], dl[r]);
                     dprime = (double)(float)dh[r] + (double)(float)dl[r];
@@ -733,24 +912,29 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         sx += __shfl_xor(sx, 16);   sx += __shfl_xor(sx, 32);
         { double o = __shfl_xor(err, 16); err = (o > err || o != o) ? o : err;
           o = __shfl_xor(err, 32); err = (o > err || o != o) ? o : err; }
+        dmax = fmax(dmax, __shfl_xor(dmax, 16)); dmax = fmax(dmax, __shfl_xor(dmax, 32));
         if (lane < 16) {
-            double* d = nred + ((long long)wm * K + rhs) * 3;
+            double* d = nred + ((long long)wm * K + rhs) * 4;
             d[0] = sbx;
             d[1] = sx;
             d[2] = err;
+            d[3] = dmax;
         }
     }
     __syncthreads();
     for (int rhs = threadIdx.x; rhs < K; rhs += T) {
-        double a = 0.0, b = 0.0, e = 0.0;
+        double a = 0.0, b = 0.0, e = 0.0, dm = 0.0;
         for (int q = 0; q < 4; ++q) {
-            const double* d = nred + ((long long)q * K + rhs) * 3;
+            const double* d = nred + ((long long)q * K + rhs) * 4;
             a += d[0];
             b += d[1];
             e = (d[2] > e || d[2] != d[2]) ? d[2] : e;
+            dm = fmax(dm, d[3]);
         }
         double* dst = p.norms + ((long long)blockIdx.x * p.k + rhs) * 4;
         dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
+        // the tile's max |D| for the e4m3 scale of the direction's lo piece in pass 2 (lo8)
+        if (p.dexp) p.dexp[(long long)blockIdx.x * p.k + rhs] = panel_frexp(dm);
     }
 }
 
@@ -759,7 +943,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
 // epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
 // per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI, int ILV, int DS, int WNX>
+template <int NT, int EPI, int ILV, int DS, int WNX, int L8 = 0>
 __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
                                                                          double* __restrict__ Gout) {
     using G = PanelGeo<NT, 2, WNX>;
@@ -769,7 +953,11 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+    if constexpr (L8)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
+        panel_mainloop_lo8<NT, 1, ILV, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
+                                            (int)(p.m / kPanelK), p.rexp, p.m / kPanelRows, 1,
+                                            (int)(p.m / kPanelRows), panel_a_exp(p.amax), acc);
+    else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                       (int)(p.m / kPanelK), acc);
     else if constexpr (ILV >= 2)
@@ -786,7 +974,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
 // pass 2: partial S over one column chunk: Sslab[chunk][rhs][row]; the direction in NS
 // bf16 pieces.  grid = (m / 256) x kchunks
 // ---------------------------------------------------------------------------
-template <int NT, int ILV, int NS, int WNX>
+template <int NT, int ILV, int NS, int WNX, int L8 = 0>
 __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(PanelParams p, int fixed_block) {
     using G = PanelGeo<NT, NS, WNX>;
     __shared__ __attribute__((aligned(16))) char smem[G::Smem];
@@ -810,7 +998,11 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
     const long long kc = p.w / p.kchunks;
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
-    if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
+    if constexpr (L8 && NS == 2)   // the direction's lo piece on e4m3: scales from the chunk's tiles' max |D|
+        panel_mainloop_lo8<NT, 2, ILV, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
+                                            chunk * kc, (int)(kc / kPanelK), p.dexp + (chunk * kc / kPanelRows) * p.k,
+                                            1, p.k, (int)(kc / kPanelRows), panel_a_exp(p.amax), acc);
+    else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);
     else if constexpr (ILV >= 2)
@@ -977,6 +1169,17 @@ __device__ __forceinline__ void panel_bump_t(const PanelParams& p, bool pending)
     }
 }
 
+// lo8: the max |R| of the 256 residual rows a wave's 64 units (4 rows each, one RHS) hold -> the
+// exponent table pass 1 scales the residual's lo piece by.  v: this lane's unit in [k][m / 4]; the
+// wave's units are v0 .. v0 + 63 with 64 | v0 (the callers' unit ranges are multiples of 64), so
+// the wave's group is v0 / 64 of [k][m / 256].  Whole waves only (wave_max).
+__device__ __forceinline__ void panel_put_rexp(const PanelParams& p, unsigned v, const double (&r)[4]) {
+    if (!p.rexp) return;
+    double mx = fmax(fmax(fabs(r[0]), fabs(r[1])), fmax(fabs(r[2]), fabs(r[3])));
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) p.rexp[v / 64] = panel_frexp(mx);
+}
+
 // x_j += gamma_j D'_j ; Ax_j += gamma_j S_j ; R = sum_b Ax_b - B ; split R.
 // Work units: u < ux -> 8 consecutive x elements ([k][w], 16-B Dh (+ Dl when DS = 2) loads);
 // ux <= u < ux + ur -> 4 consecutive residual rows ([k][m]).  Also bumps t.  k*w and k*m <
@@ -1054,6 +1257,7 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
             wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
             wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
             wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+            panel_put_rexp(p, v, r);
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, false);
@@ -1083,6 +1287,7 @@ __global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p) {
         wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
         wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
         wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+        panel_put_rexp(p, v, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, true);
 }
@@ -1143,14 +1348,20 @@ __global__ __launch_bounds__(kThreads) void k_panel_diag(PanelParams p, double* 
     const long long n = (long long)p.nblock * p.w;
     const long long col = (long long)blockIdx.x * 512 + lane * 8;
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float amax = 0.0f;
     for (long long i = wave; i < p.m && col < n; i += kWaves) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(p.A + i * p.lda + col);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const double d = (double)(float)v[e];
             acc[e] = fma(d, d, acc[e]);
+            amax = fmaxf(amax, fabsf((float)v[e]));
         }
     }
+    // max |A| for the e4m3 image of A (lo8): non-negative floats order as their bit patterns
+    amax = (float)wave_max((double)amax);
+    if (p.amax && lane == 0 && amax > 0.0f)
+        __hip_atomic_fetch_max(p.amax, __float_as_uint(amax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ double part[kWaves][512];
 #pragma unroll
     for (int e = 0; e < 8; ++e) part[wave][lane * 8 + e] = acc[e];
@@ -1159,6 +1370,99 @@ __global__ __launch_bounds__(kThreads) void k_panel_diag(PanelParams p, double* 
         const double s = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
         diag[blockIdx.x * 512 + c] = s;
         rec[blockIdx.x * 512 + c] = 1.0 / s;
+    }
+}
+
+// lo8: the exponent table of the residual p.R (reset and refresh; the update kernels keep it
+// current every iteration).  A thread owns 4 consecutive rows, a wave 256 rows of one RHS.
+__global__ __launch_bounds__(kThreads) void k_panel_rexp(PanelParams p) {
+    const unsigned ur = (unsigned)((long long)p.k * p.m / 4);
+    for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
+        const double2 r01 = *reinterpret_cast<const double2*>(p.R + 4ll * v);
+        const double2 r23 = *reinterpret_cast<const double2*>(p.R + 4ll * v + 2);
+        const double r[4] = {r01.x, r01.y, r23.x, r23.y};
+        panel_put_rexp(p, v, r);
+    }
+}
+
+// Exact residual refresh (lo8): the incremental R += gamma S drifts from B - A X by the e4m3 lo
+// product's error (S = A_hi D_hi + A8 D_lo8 != A D'), so every "r_refresh" iterations R is
+// recomputed from X.  X (fp32) = Xh + Xm + Xl exactly in three bf16 pieces (8 + 8 + 8 significant
+// bits); pass 2 multiplies (Xh, Xm) as its usual hi + lo pair and Xl as a one-piece operand, fp32
+// accumulation per column chunk, fp64 across chunks (k_panel_refresh_fin).
+__global__ __launch_bounds__(kThreads) void k_panel_xsplit3(PanelParams p, int block, __bf16* __restrict__ h,
+                                                            __bf16* __restrict__ m, __bf16* __restrict__ l) {
+    const long long nx = (long long)p.k * p.w;
+    for (long long e = (long long)blockIdx.x * kThreads + threadIdx.x; e < nx; e += (long long)gridDim.x * kThreads) {
+        const float x = p.X[(long long)block * nx + e];
+        const long long rhs = e / p.w;
+        const long long d = rhs * p.ldd + (e - rhs * p.w);
+        const __bf16 xh = to_bf16(x);
+        const float r1 = x - (float)xh;   // exact
+        const __bf16 xm = to_bf16(r1);
+        h[d] = xh;
+        m[d] = xm;
+        l[d] = to_bf16(r1 - (float)xm);   // exact: at most 8 significant bits remain
+    }
+}
+// acc = S (the (Xh, Xm) product, k_panel_reduce mode 0) + sum_c Sslab[c] (the Xl product);
+// one feature block: R = acc - B, its hi / lo split and exponent table; several: Ax_block = acc
+// (R then follows from all blocks, k_panel_r_from_ax).  A thread owns 4 consecutive rows.
+__global__ __launch_bounds__(kThreads) void k_panel_refresh_fin(PanelParams p, int block) {
+    const long long nr = (long long)p.k * p.m;
+    const unsigned ur = (unsigned)(nr / 4), m4 = (unsigned)(p.m / 4);
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+    for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
+        const long long e = 4ll * v;
+        double a[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = p.S[e + q];
+        for (int c = 0; c < p.kchunks; ++c) {
+            const float4 s = *reinterpret_cast<const float4*>(p.Sslab + (long long)c * nr + e);
+            a[0] += (double)s.x; a[1] += (double)s.y; a[2] += (double)s.z; a[3] += (double)s.w;
+        }
+        if (p.nblock == 1) {
+            const unsigned rhs = v / m4;
+            const long long re = (long long)rhs * p.ldr + (e - (long long)rhs * p.m);
+            double r[4];
+            __bf16 hi[4], lo[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                r[q] = a[q] - p.B[e + q];
+                split_bf16(r[q], hi[q], lo[q]);
+                p.R[e + q] = r[q];
+            }
+            *reinterpret_cast<bf16x4v*>(p.Rh + re) = bf16x4v{hi[0], hi[1], hi[2], hi[3]};
+            *reinterpret_cast<bf16x4v*>(p.Rl + re) = bf16x4v{lo[0], lo[1], lo[2], lo[3]};
+            panel_put_rexp(p, v, r);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) p.Ax[(long long)block * nr + e + q] = a[q];
+        }
+    }
+}
+// several feature blocks, after every block's refresh: R = sum_b Ax_b - B, split, exponent table
+__global__ __launch_bounds__(kThreads) void k_panel_r_from_ax(PanelParams p) {
+    const long long nr = (long long)p.k * p.m;
+    const unsigned ur = (unsigned)(nr / 4), m4 = (unsigned)(p.m / 4);
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+    for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
+        const long long e = 4ll * v;
+        const unsigned rhs = v / m4;
+        const long long re = (long long)rhs * p.ldr + (e - (long long)rhs * p.m);
+        double r[4];
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double acc = p.Ax[e + q];
+            for (int b = 1; b < p.nblock; ++b) acc += p.Ax[(long long)b * nr + e + q];
+            r[q] = acc - p.B[e + q];
+            split_bf16(r[q], hi[q], lo[q]);
+            p.R[e + q] = r[q];
+        }
+        *reinterpret_cast<bf16x4v*>(p.Rh + re) = bf16x4v{hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<bf16x4v*>(p.Rl + re) = bf16x4v{lo[0], lo[1], lo[2], lo[3]};
+        panel_put_rexp(p, v, r);
     }
 }
 

@@ -38,6 +38,11 @@ struct bpgl_panel {
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
+    int lo8 = 0;                  // e4m3 lo products ("lo8" knob): bit 0 pass 1 (residual), bit 1 pass 2 (direction)
+    int64_t r_period = 128;       // exact residual refresh every r_period iterations when pass 2 runs lo8 ("r_refresh")
+    int64_t t_host = 0;           // iterations enqueued since the last reset
+    int64_t last_refresh = 0;     // t_host of the last refresh
+    int64_t n_refresh = 0;        // refreshes since the last reset
     int64_t ldr() const { return m + op_pad; }
     int64_t ldd() const { return w + op_pad; }
 };
@@ -45,7 +50,8 @@ struct bpgl_panel {
 namespace {
 
 struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, total;
+    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, amax, rexp, dexp,
+        X3, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -70,12 +76,44 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.gamma = k.take(8 * c->k);
     L.err_rhs = k.take(8 * c->k);
     L.cnt = k.take(8 * c->k);
+    L.amax = k.take(8);
+    L.rexp = k.take(4 * (int64_t)c->k * (c->m / kPanelRows));
+    L.dexp = k.take(4 * (c->w / kPanelRows) * (int64_t)c->k);
+    L.X3 = k.take(2 * (int64_t)c->k * c->ldd());   // the third bf16 piece of X (residual refresh)
     L.total = k.off;
     return L;
 }
 
 // ns: bf16 pieces of the direction (pass 1's epilogue writes it, pass 2 reads it): the
 // solver's d_split knob, 2 for the API products (bpgl_panel_mtm / _mm)
+// lo8 forms: 8 waves (WNX 0), mainloop ILV 0 / 1 (pass 1's default pipe form falls back to ILV 1)
+template <int NT, int NS>
+int panel_launch_lo8(bpgl_panel* c, int which) {
+    const bool i0 = c->interleave[which] == 0;
+    if (which == 0) {
+        if (i0) hipLaunchKernelGGL((k_panel_pass1<NT, 1, 0, NS, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
+                                   dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1, nullptr);
+        else hipLaunchKernelGGL((k_panel_pass1<NT, 1, 1, NS, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
+                                dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1, nullptr);
+        LAUNCH_CHECK("k_panel_pass1");
+    } else {
+        const dim3 g((unsigned)((c->m / kPanelRows) * c->kchunks));
+        if (i0) hipLaunchKernelGGL((k_panel_pass2<NT, 0, 2, 0, 1>), g, dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1);
+        else hipLaunchKernelGGL((k_panel_pass2<NT, 1, 2, 0, 1>), g, dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1);
+        LAUNCH_CHECK("k_panel_pass2");
+    }
+    return 0;
+}
+template <int NS>
+int panel_launch_lo8_ns(bpgl_panel* c, int which) {
+    switch (c->k) {
+        case 16: return panel_launch_lo8<1, NS>(c, which);
+        case 32: return panel_launch_lo8<2, NS>(c, which);
+        case 64: return panel_launch_lo8<4, NS>(c, which);
+        default: return panel_launch_lo8<8, NS>(c, which);
+    }
+}
+
 template <int NT, int ILV, int NS, int WNX>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
@@ -125,6 +163,12 @@ int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mod
     return ns == 1 ? panel_launch_ns<1>(c, which, fixed_block, out, mode)
                    : panel_launch_ns<2>(c, which, fixed_block, out, mode);
 }
+// a solver pass: the lo8 form when the knob selects it for this pass (pass 2 needs the hi + lo direction)
+int panel_pass(bpgl_panel* c, int which) {
+    const bool l8 = which == 0 ? (c->lo8 & 1) != 0 : ((c->lo8 & 2) != 0 && c->dsplit == 2);
+    if (l8) return c->dsplit == 1 ? panel_launch_lo8_ns<1>(c, which) : panel_launch_lo8_ns<2>(c, which);
+    return panel_launch(c, which, -1, nullptr, 1, c->dsplit);
+}
 int panel_reduce(bpgl_panel* c, double* out, int mode) {
     hipLaunchKernelGGL(k_panel_reduce, dim3((unsigned)(c->k * cdiv(c->m, kLspRows))), dim3(kThreads), 0, c->stream,
                        c->p, out, mode);
@@ -145,10 +189,10 @@ void panel_ev(bpgl_panel* c, int64_t it, int kind, int end) {
 int panel_iteration(bpgl_panel* c, int64_t it) {
     int rc;
     panel_ev(c, it, 0, 0);
-    if ((rc = panel_launch(c, 0, -1, nullptr, 1, c->dsplit))) return rc;
+    if ((rc = panel_pass(c, 0))) return rc;
     panel_ev(c, it, 0, 1);
     panel_ev(c, it, 1, 0);
-    if ((rc = panel_launch(c, 1, -1, nullptr, 1, c->dsplit))) return rc;
+    if ((rc = panel_pass(c, 1))) return rc;
     panel_ev(c, it, 1, 1);
     panel_ev(c, it, 2, 0);
     if ((rc = panel_reduce(c, c->p.S, 1))) return rc;   // its last block per RHS runs the line search
@@ -182,6 +226,51 @@ int panel_split(bpgl_panel* c, const double* src, int64_t len, int64_t ld, __bf1
     LAUNCH_CHECK("k_panel_split");
     return 0;
 }
+// exact residual refresh (lo8 in pass 2; bpgl_panel.h k_panel_xsplit3): R = A X - B from X's three
+// bf16 pieces, per feature block, then the residual's split and exponent table
+int panel_refresh(bpgl_panel* c) {
+    PanelParams& p = c->p;
+    const int64_t nx = (int64_t)c->k * c->w, nr = (int64_t)c->k * c->m;
+    if (c->defer_x) {   // x += gamma D' of the last iteration first: X must be current
+        const dim3 fg((unsigned)std::min<int64_t>(cdiv(nx / 8, kThreads), 8192));
+        if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_flush<1>, fg, dim3(kThreads), 0, c->stream, p);
+        else hipLaunchKernelGGL(k_panel_flush<2>, fg, dim3(kThreads), 0, c->stream, p);
+        LAUNCH_CHECK("k_panel_flush");
+        hipLaunchKernelGGL(k_panel_clear_pending, dim3(1), dim3(64), 0, c->stream, p);
+        LAUNCH_CHECK("k_panel_clear_pending");
+    }
+    __bf16* x3 = (__bf16*)((char*)p.st + (panel_layout(c).X3 - panel_layout(c).st));
+    const dim3 eg((unsigned)std::min<int64_t>(cdiv(nx, kThreads), 8192));
+    const dim3 rg((unsigned)std::min<int64_t>(cdiv(nr / 4, kThreads), 8192));
+    int rc;
+    for (int b = 0; b < c->nblock; ++b) {
+        hipLaunchKernelGGL(k_panel_xsplit3, eg, dim3(kThreads), 0, c->stream, p, b, p.Dh, p.Dl, x3);
+        LAUNCH_CHECK("k_panel_xsplit3");
+        if ((rc = panel_launch(c, 1, b, nullptr, 0, 2))) return rc;   // (Xh, Xm) -> slab
+        if ((rc = panel_reduce(c, p.S, 0))) return rc;                // -> S
+        __bf16* dh = p.Dh;
+        p.Dh = x3;                                                    // Xl alone -> slab
+        rc = panel_launch(c, 1, b, nullptr, 0, 1);
+        p.Dh = dh;
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_panel_refresh_fin, rg, dim3(kThreads), 0, c->stream, p, b);
+        LAUNCH_CHECK("k_panel_refresh_fin");
+    }
+    if (c->nblock > 1) {
+        hipLaunchKernelGGL(k_panel_r_from_ax, rg, dim3(kThreads), 0, c->stream, p);
+        LAUNCH_CHECK("k_panel_r_from_ax");
+    }
+    c->n_refresh++;
+    c->last_refresh = c->t_host;
+    return 0;
+}
+int panel_rexp(bpgl_panel* c) {
+    const dim3 rg((unsigned)std::min<int64_t>(cdiv((int64_t)c->k * c->m / 4, kThreads), 8192));
+    hipLaunchKernelGGL(k_panel_rexp, rg, dim3(kThreads), 0, c->stream, c->p);
+    LAUNCH_CHECK("k_panel_rexp");
+    return 0;
+}
+
 int panel_ready(const bpgl_panel* c) {
     if (!c) return fail(BPGL_E_ARG, "null panel context");
     if (!c->bound) return fail(BPGL_E_STATE, "bpgl_panel_bind has not been called");
@@ -203,9 +292,9 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
                                               kPanelRows);
     if (w <= 0 || w % kPanelRows) return fail(BPGL_E_ARG, "block width (%lld) must be a positive multiple of %d",
                                               (long long)w, kPanelRows);
-    if (kchunks <= 0) {   // one pass-2 tile per CU (256), chunk width a multiple of the 64-deep stage
-        kchunks = (int32_t)std::max<int64_t>(1, std::min<int64_t>(w / kPanelK, 256 / (m / kPanelRows)));
-        while (w % ((int64_t)kchunks * kPanelK)) --kchunks;
+    if (kchunks <= 0) {   // one pass-2 tile per CU (256), chunk width a multiple of two 64-deep stages (lo8)
+        kchunks = (int32_t)std::max<int64_t>(1, std::min<int64_t>(w / (2 * kPanelK), 256 / (m / kPanelRows)));
+        while (kchunks > 1 && w % ((int64_t)kchunks * 2 * kPanelK)) --kchunks;
     }
     if (w % ((int64_t)kchunks * kPanelK)) return fail(BPGL_E_ARG, "w must be a multiple of 64 * kchunks");
     if ((int64_t)nrhs * w >= (1ll << 31) || (int64_t)nrhs * m >= (1ll << 31))
@@ -283,6 +372,9 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.gamma = (double*)(s + L.gamma);
     p.err_rhs = (double*)(s + L.err_rhs);
     p.cnt = (unsigned long long*)(s + L.cnt);
+    p.amax = (unsigned*)(s + L.amax);
+    p.rexp = (int*)(s + L.rexp);
+    p.dexp = (int*)(s + L.dexp);
     p.wt = c->wt;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
@@ -297,6 +389,7 @@ int bpgl_panel_diag(bpgl_panel* c, double* out) {
     int rc;
     if ((rc = panel_ready(c))) return rc;
     HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemsetAsync(c->p.amax, 0, sizeof(unsigned), c->stream));
     hipLaunchKernelGGL(k_panel_diag, dim3((unsigned)cdiv(c->n, 512)), dim3(kThreads), 0, c->stream, c->p,
                        const_cast<double*>(c->p.diag), const_cast<double*>(c->p.rec));
     LAUNCH_CHECK("k_panel_diag");
@@ -343,6 +436,10 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     HIP_TRY(hipMemsetAsync(p.Ax, 0, 8 * km * c->nblock, c->stream));
     // x = 0 => Ax = 0, R = -B
     if ((rc = panel_split(c, p.B, c->m, c->ldr(), p.Rh, p.Rl, -1.0, p.R))) return rc;
+    if ((rc = panel_rexp(c))) return rc;
+    c->t_host = 0;
+    c->last_refresh = 0;
+    c->n_refresh = 0;
     p.err_iter = err_iter;
     p.rec_len = err_iter ? record_len : 0;
     hipLaunchKernelGGL(k_panel_reset_state, dim3(1), dim3(64), 0, c->stream, c->p);
@@ -376,12 +473,23 @@ int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
     if ((rc = panel_ready(c))) return rc;
     if (!c->solver) return fail(BPGL_E_STATE, "bpgl_panel_reset has not been called");
     HIP_TRY(hipSetDevice(c->device));
+    // lo8 in pass 2: an exact residual refresh every r_period iterations (between graph replays;
+    // r_period is a multiple of the graph length, so no replay crosses one)
+    const bool refresh = (c->lo8 & 2) && c->dsplit == 2 && c->r_period > 0;
     int64_t i = 0;
-    if (!c->timing && c->gexec)
-        for (; i + kGraphIters <= n_iter; i += kGraphIters) HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
-    for (; i < n_iter; ++i) {
-        if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
-        if (c->timing) c->timed_iters++;
+    while (i < n_iter) {
+        if (refresh && c->t_host > 0 && c->t_host % c->r_period == 0 && c->last_refresh != c->t_host)
+            if ((rc = panel_refresh(c))) return rc;
+        if (!c->timing && c->gexec && i + kGraphIters <= n_iter && c->t_host % kGraphIters == 0) {
+            HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
+            i += kGraphIters;
+            c->t_host += kGraphIters;
+        } else {
+            if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
+            if (c->timing) c->timed_iters++;
+            ++i;
+            ++c->t_host;
+        }
     }
     if (c->nblock == 1 && c->defer_x) {   // the last iteration's x update, so X is current between calls
         const dim3 fg((unsigned)std::min<int64_t>(cdiv((int64_t)c->k * c->w / 8, kThreads), 8192));
@@ -458,6 +566,18 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;
+    } else if (!strcmp(key, "lo8")) {
+        if (value < 0 || value > 3) return fail(BPGL_E_ARG, "lo8 is a mask: 1 pass 1 (residual), 2 pass 2 (direction)");
+        if ((value & 2) && (c->w / c->kchunks) % (2 * kPanelK))
+            return fail(BPGL_E_ARG, "lo8 in pass 2 needs a column chunk (w / kchunks) that is a multiple of %d",
+                        2 * kPanelK);
+        c->lo8 = (int)value;
+        c->solver = false;   // the refresh schedule restarts with the solve: a reset must follow
+    } else if (!strcmp(key, "r_refresh")) {
+        if (value < 0 || value % kGraphIters)
+            return fail(BPGL_E_ARG, "r_refresh must be 0 (never) or a positive multiple of %d", kGraphIters);
+        c->r_period = value;
+        return 0;
     } else if (!strcmp(key, "op_pad")) {   // changes the scratch layout: only before bpgl_panel_bind
         if (c->bound) return fail(BPGL_E_STATE, "op_pad must be set before bpgl_panel_bind");
         if (value < 0 || value % 64 || value > 4096)
@@ -483,8 +603,28 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "write_through")) *value = c->wt;
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else if (!strcmp(key, "op_pad")) *value = c->op_pad;
+    else if (!strcmp(key, "lo8")) *value = c->lo8;
+    else if (!strcmp(key, "r_refresh")) *value = c->r_period;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;
+}
+
+int bpgl_panel_stat(const bpgl_panel* c, const char* key, int64_t* value) {
+    if (!c || !key || !value) return fail(BPGL_E_ARG, "null argument");
+    if (!strcmp(key, "refreshes")) *value = c->n_refresh;
+    else if (!strcmp(key, "iters_enqueued")) *value = c->t_host;
+    else return fail(BPGL_E_ARG, "unknown panel stat '%s'", key);
+    return 0;
+}
+
+const double* bpgl_panel_residual(bpgl_panel* c) { return c ? c->p.R : nullptr; }
+
+int bpgl_panel_refresh(bpgl_panel* c) {
+    int rc;
+    if ((rc = panel_ready(c))) return rc;
+    if (!c->solver) return fail(BPGL_E_STATE, "bpgl_panel_reset has not been called");
+    HIP_TRY(hipSetDevice(c->device));
+    return panel_refresh(c);
 }
 
 int bpgl_panel_geometry(const bpgl_panel* c, int32_t* kchunks) {

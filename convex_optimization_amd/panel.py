@@ -44,6 +44,9 @@ _PANEL_SIGS = {
     "bpgl_panel_geometry": (ctypes.c_int, [_p, ctypes.POINTER(_i32)]),
     "bpgl_panel_set_tuning": (ctypes.c_int, [_p, ctypes.c_char_p, _i64]),
     "bpgl_panel_get_tuning": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(_i64)]),
+    "bpgl_panel_stat": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(_i64)]),
+    "bpgl_panel_residual": (_p, [_p]),
+    "bpgl_panel_refresh": (ctypes.c_int, [_p]),
 }
 N._SIGS.update(_PANEL_SIGS)
 
@@ -196,6 +199,24 @@ class PanelLasso:
         v = ctypes.c_int64()
         N.check(_lib().bpgl_panel_get_tuning(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_panel_get_tuning")
         return v.value
+
+    def stat(self, key):
+        """Counter since the last reset: "refreshes", "iters_enqueued"."""
+        v = ctypes.c_int64()
+        N.check(_lib().bpgl_panel_stat(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_panel_stat")
+        return v.value
+
+    def residual_device(self):
+        """(k, m) fp64 device view of the solver's residual R = A X - B (drain the stream first)."""
+        addr = _lib().bpgl_panel_residual(self._ctx)
+        off = addr - self._scratch.data_ptr()
+        assert off % 8 == 0
+        return self._scratch[off // 8: off // 8 + self.nrhs * self.MAT_HEIGHT].view(self.nrhs, self.MAT_HEIGHT)
+
+    def refresh(self):
+        """Recompute the residual exactly from X (the lo8 refresh) now."""
+        with self._on_stream():
+            N.check(_lib().bpgl_panel_refresh(self._ctx), "bpgl_panel_refresh")
 
     def set_kernel_timing(self, enable):
         N.check(_lib().bpgl_panel_set_kernel_timing(self._ctx, int(bool(enable))), "bpgl_panel_set_kernel_timing")

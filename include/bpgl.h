@@ -332,9 +332,25 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * rounding alone (half the pass-2 MFMA work).  bpgl_panel_mtm / _mm always use
  * hi + lo operands.  bpgl_panel_get_tuning reads "interleave1", "interleave2",
  * "d_split". */
+/* "lo8" (mask; a reset must follow): the lo piece of the residual (bit 0, pass 1) and
+ * of the direction (bit 1, pass 2) on block-scaled e4m3 MFMA
+ * (v_mfma_scale_f32_16x16x128_f8f6f4, twice the bf16 rate) against an e4m3 image of
+ * A, the hi piece on bf16 as before: operands to ~2^-13 instead of ~2^-17.  With
+ * bit 1 the product S no longer equals A D' exactly, so the incrementally updated
+ * residual is recomputed exactly (R = A X - B from X's three bf16 pieces) every
+ * "r_refresh" iterations (default 128; 0 = never; a multiple of 8).  lo8 passes use
+ * the interleave 0 / 1 mainloops (2 and 3 fall back to 1) with 8 waves. */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_get_tuning(const bpgl_panel* ctx, const char* key, int64_t* value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
+/* Counters since the last reset: "refreshes" (exact residual refreshes run),
+ * "iters_enqueued". */
+int bpgl_panel_stat(const bpgl_panel* ctx, const char* key, int64_t* value);
+/* The solver's fp64 residual R = A X - B, [nrhs][m] in device memory (valid after
+ * the stream has drained). */
+const double* bpgl_panel_residual(bpgl_panel* ctx);
+/* Recompute R exactly from X now (the lo8 refresh; any lo8 setting). */
+int bpgl_panel_refresh(bpgl_panel* ctx);
 
 #ifdef __cplusplus
 }

@@ -248,3 +248,103 @@ def test_panel_full_configs4_shape_matches_oracle():
         assert ex <= 1e-3, ex
         f_dev, f_ref = objective(Ah, Bh[:, j], mu[j], X[:, j]), objective(Ah, Bh[:, j], mu[j], ref)
         assert abs(f_dev - f_ref) <= 1e-5 * f_ref, (j, abs(f_dev - f_ref) / f_ref)
+
+
+def _residual_drift(pl, Ab, B):
+    """max |R_device - (A X - B)| / max |A X - B| over all RHS (fp64 on the host)"""
+    torch.cuda.synchronize()
+    pl.stream.synchronize()
+    R = pl.residual_device().t().cpu().numpy()
+    Rex = Ab @ pl.solver_x() - B
+    return np.abs(R - Rex).max() / np.abs(Rex).max()
+
+
+@pytest.mark.parametrize("lo8,rr", [(1, 0), (2, 16), (3, 16), (3, 0)])
+@pytest.mark.parametrize("m,n,blocks,k,iters", [(512, 2048, 1, 32, 150), (512, 1024, 1, 128, 60),
+                                                (256, 1024, 2, 64, 80)])
+def test_panel_lo8_solver_matches_per_rhs_oracle(m, n, blocks, k, iters, lo8, rr):
+    """The e4m3 lo products (lo8 bit 0: the residual's lo piece in pass 1; bit 1: the direction's in
+    pass 2, with the exact residual refresh every rr iterations) meet the path's stated tolerance
+    against the per-RHS fp64 oracle on the same bf16 A: x within 1e-2 relative l2, objective within
+    1e-5 relative."""
+    Ab, B, mu = instance(m, n, k, seed=7 + k)
+    pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
+    pl.set_tuning("lo8", lo8)
+    pl.set_tuning("r_refresh", rr)
+    assert (pl.get_tuning("lo8"), pl.get_tuning("r_refresh")) == (lo8, rr)
+    res = pl.run(B, mu, iters, record=True)
+    assert res["iters"] == iters
+    assert pl.stat("refreshes") == ((iters - 1) // rr if rr and lo8 & 2 else 0)
+    X = res["x"]
+    worst_x, worst_f = 0.0, 0.0
+    for j in range(0, k, max(1, k // 8)):
+        ref = oracle.run(Ab, B[:, j], mu[j], blocks, iters, nthreads=NT)["x"]
+        worst_x = max(worst_x, np.linalg.norm(X[:, j] - ref) / np.linalg.norm(ref))
+        f_dev, f_ref = objective(Ab, B[:, j], mu[j], X[:, j]), objective(Ab, B[:, j], mu[j], ref)
+        worst_f = max(worst_f, abs(f_dev - f_ref) / f_ref)
+    print(f"panel lo8={lo8} r_refresh={rr} m={m} n={n} k={k}: worst rel x {worst_x:.2e}, objective {worst_f:.2e}")
+    assert worst_x <= 1e-2
+    assert worst_f <= 1e-5
+    assert np.all(np.isfinite(res["err_iter"]))
+
+
+def test_panel_lo8_graph_equals_eager():
+    """Graph replay and eager launches run the same lo8 kernels and the same refresh schedule (the
+    refresh runs between replays): bitwise equal iterates."""
+    Ab, B, mu = instance(512, 1024, 128, seed=4)
+    pl = PanelLasso(Ab, 1, nrhs=128, device=0)
+    pl.set_tuning("lo8", 3)
+    pl.set_tuning("r_refresh", 16)
+    a = pl.run(B, mu, 44, use_graph=True)["x"]
+    assert pl.stat("refreshes") == 2
+    b = pl.run(B, mu, 44, use_graph=False)["x"]
+    np.testing.assert_array_equal(a, b)
+    pl.solver_reset(B, mu)                      # split step calls: the schedule follows the iteration count
+    for n_it in (5, 3, 16, 9, 11):
+        pl.solver_step(n_it)
+    np.testing.assert_array_equal(pl.solver_x(), a)
+
+
+def test_panel_lo8_residual_refresh_pins_the_drift():
+    """lo8 in pass 2 makes the product S = A_hi D_hi + A8 D_lo8 differ from A D' (the direction the
+    update applies) by the e4m3 lo term's rounding, so the incrementally updated residual drifts
+    from A X - B; the refresh recomputes it from X's three exact bf16 pieces.  Measured here: the
+    drift without refreshes after 60 iterations is above the bf16 form's (fp32 accumulation only)
+    and below 1e-3 of max |R|; right after a refresh it is back below 1e-6 (fp32 accumulation over
+    a column chunk)."""
+    Ab, B, mu = instance(512, 2048, 64, seed=17)
+    pl = PanelLasso(Ab, 1, nrhs=64, device=0)
+    pl.solver_reset(B, mu)
+    pl.solver_step(60)
+    d_bf16 = _residual_drift(pl, Ab, B)
+    pl.set_tuning("lo8", 2)
+    pl.set_tuning("r_refresh", 0)
+    pl.solver_reset(B, mu)
+    pl.solver_step(60)
+    d_lo8 = _residual_drift(pl, Ab, B)
+    pl.refresh()
+    d_after = _residual_drift(pl, Ab, B)
+    print(f"residual drift after 60 iterations: bf16 {d_bf16:.2e}, lo8 {d_lo8:.2e}, lo8 after refresh {d_after:.2e}")
+    assert d_lo8 <= 1e-3
+    assert d_after <= 1e-6
+    assert d_after < d_lo8
+    pl.solver_step(20)                        # the solve continues from the refreshed residual
+    assert np.all(np.isfinite(pl.solver_x()))
+
+
+def test_panel_lo8_knob_errors():
+    Ab, B, mu = instance(256, 512, 16, seed=2)
+    pl = PanelLasso(Ab, 1, nrhs=16, device=0, kchunks=8)   # 64-column chunks: too narrow for lo8 in pass 2
+    with pytest.raises(Exception):
+        pl.set_tuning("lo8", 2)
+    pl.set_tuning("lo8", 1)
+    with pytest.raises(Exception):
+        pl.set_tuning("lo8", 4)
+    with pytest.raises(Exception):
+        pl.set_tuning("r_refresh", 12)       # not a multiple of the 8-iteration graph
+    pl.solver_reset(B, mu)
+    pl.solver_step(2)
+    pl.set_tuning("lo8", 0)
+    with pytest.raises(Exception):
+        pl.solver_step(1)                    # a lo8 change needs a reset
+    assert PanelLasso(Ab, 1, nrhs=16, device=0).kchunks == 4   # the automatic chunks fit lo8 (128 | w / kchunks)

@@ -5,6 +5,7 @@
 set -o pipefail
 OUT=gpurun_out/r04_multi
 mkdir -p $OUT
+timeout -k 10 60 tools/_mfma_f8_probe > $OUT/mfma_f8_probe.txt 2>&1 &&
 timeout -k 10 60 tools/_cumask_probe > $OUT/cumask_probe.txt 2>&1 &&
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_ranks.py \
     -k "8 or collective" > $OUT/pytest_rccl8.txt 2>&1 &&
