@@ -657,6 +657,30 @@ __device__ __forceinline__ int panel_a_exp(const unsigned* amax) {
     return panel_clamp_exp(e - 8);
 }
 
+// lane scales of the lo piece: lane l reduces the exponents of RHS wn * RW + l % RW (RW = the wave's
+// RHS), then N-tile nt takes lane nt * 16 + (l & 15)'s result.  All loads are issued before the
+// reduction.  esrc: the pass's exponent table, RHS r over ent entries at esrc[r * erstride + t * etstride].
+template <int NTW>
+__device__ __forceinline__ void panel_lane_scales(const int* __restrict__ esrc, long long erstride, long long etstride,
+                                                  int ent, int wn, int lane, float (&b_sc)[NTW], int (&b_e8)[NTW]) {
+    constexpr int RW = NTW * 16;
+    int emax = kExpZero;
+    const int* er = esrc + (long long)(wn * RW + lane % RW) * erstride;
+    for (int t0 = 0; t0 < ent; t0 += 32) {
+        int ev[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) ev[t] = t0 + t < ent ? er[(long long)(t0 + t) * etstride] : kExpZero;
+#pragma unroll
+        for (int t = 0; t < 32; ++t) emax = ev[t] > emax ? ev[t] : emax;
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+        const int sb = panel_lo_exp(__shfl(emax, nt * 16 + (lane & 15)));
+        b_sc[nt] = ldexpf(1.0f, sb);
+        b_e8[nt] = 127 + sb;
+    }
+}
+
 // The ILV 0 / 1 mainloop (panel_mainloop) with the lo product on e4m3, stages taken in pairs
 // (nsteps must be even: the host requires 128 | the pass's K range).  esrc: this pass's exponent
 // table, lane RHS r over ent entries at esrc[r * erstride + t * etstride]; the lane scale is the
@@ -678,28 +702,9 @@ __device__ __forceinline__ void panel_mainloop_lo8(char* smem, const __bf16* __r
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // lane scales: lane l reduces the exponents of RHS wn * RW + l % RW (RW = this wave's RHS), then
-    // N-tile nt takes lane nt * 16 + (l & 15)'s result.  All loads are issued before the reduction.
-    constexpr int RW = G::NTW * 16;
-    int emax = kExpZero;
-    {
-        const int* er = esrc + (long long)(wn * RW + lane % RW) * erstride;
-        for (int t0 = 0; t0 < ent; t0 += 32) {
-            int ev[32];
-#pragma unroll
-            for (int t = 0; t < 32; ++t) ev[t] = t0 + t < ent ? er[(long long)(t0 + t) * etstride] : kExpZero;
-#pragma unroll
-            for (int t = 0; t < 32; ++t) emax = ev[t] > emax ? ev[t] : emax;
-        }
-    }
     float b_sc[G::NTW];
     int b_e8[G::NTW];
-#pragma unroll
-    for (int nt = 0; nt < G::NTW; ++nt) {
-        const int sb = panel_lo_exp(__shfl(emax, nt * 16 + (lane & 15)));
-        b_sc[nt] = ldexpf(1.0f, sb);
-        b_e8[nt] = 127 + sb;
-    }
+    panel_lane_scales<G::NTW>(esrc, erstride, etstride, ent, wn, lane, b_sc, b_e8);
     const float a_sc = ldexpf(1.0f, a_exp);
     const int a_e8 = 127 + a_exp;
 
@@ -777,6 +782,122 @@ __device__ __forceinline__ void panel_mainloop_lo8(char* smem, const __bf16* __r
             });
         });
         abuf = abuf == 2 ? 0 : abuf + 1;
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+        stage(s, std::integral_constant<int, 0>{});
+        stage(s + 1, std::integral_constant<int, 1>{});
+    }
+    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
+}
+
+// The software-pipelined mainloop (panel_mainloop_pipe, interleave 2: fragments read one MFMA group
+// ahead, the stage barrier before a stage's last group) with the lo product on e4m3, stages in pairs.
+// A's fragments of K-half h are converted at the group that first uses them (nt = 0), a lo fragment
+// at its own group; the e4m3 MFMAs of N-tile nt follow its hi MFMAs in the group (odd stage, h = 1).
+template <int NT, int PASS, int WNX>
+__device__ __forceinline__ void panel_mainloop_pipe_lo8(char* smem, const __bf16* __restrict__ A, long long lda,
+                                                        long long a_row0, long long a_col0,
+                                                        const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
+                                                        long long ldb, long long b_k0, int nsteps,
+                                                        const int* __restrict__ esrc, long long erstride,
+                                                        long long etstride, int ent, int a_exp,
+                                                        f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
+    using G = PanelGeo<NT, 2, WNX>;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 3, wn = wave >> 2;
+    char* abufs = smem;
+    char* obufs = smem + kPanelNA * kPanelAStage;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float b_sc[G::NTW];
+    int b_e8[G::NTW];
+    panel_lane_scales<G::NTW>(esrc, erstride, etstride, ent, wn, lane, b_sc, b_e8);
+    const float a_sc = ldexpf(1.0f, a_exp);
+    const int a_e8 = 127 + a_exp;
+    auto piece = [&](int i, int so, int bo, int sa, int ba) {
+        if (i < G::LO) {
+            panel_op_piece<NT, 2, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
+                                       lane);
+        } else if (PASS == 1) {
+            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+                                    abufs + ba * kPanelAStage, wave, lane);
+        } else {
+            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+                                    abufs + ba * kPanelAStage, wave, lane);
+        }
+    };
+    constexpr int NP = G::LO + G::LA;
+    constexpr int NG = 2 * G::NTW;
+    constexpr int NGI = NG > 1 ? NG - 1 : 1;
+    constexpr int PPG = (NP + NGI - 1) / NGI;
+    auto read_a = [&](const char* ab, int h, bf16x8 (&af)[4]) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+            af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
+                               : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
+    };
+    auto read_b = [&](const char* ob, int h, int nt, bf16x8& bhi, bf16x8& blo) {
+        const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
+        bhi = panel_bfrag(ob, rhs, h, lane);
+        blo = panel_bfrag(ob, G::K + rhs, h, lane);
+    };
+    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
+    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
+    wait_vm_barrier<G::LA>();
+    bf16x8 af[2][4];
+    bf16x8 bfr[2][2];
+    read_a(abufs, 0, af[0]);
+    read_b(obufs, 0, 0, bfr[0][0], bfr[0][1]);
+    i32x8 a8[4], b8[G::NTW];
+    int abuf = 0;
+    auto stage = [&](int s, auto parc) {
+        constexpr int par = decltype(parc)::value;
+        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
+        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
+        const int abuf_next = abuf == 2 ? 0 : abuf + 1;
+        const char* ab = abufs + abuf * kPanelAStage;
+        const char* ob = obufs + (s & 1) * G::OStage;
+        static_for<0, NG>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            constexpr int h = g / G::NTW, nt = g % G::NTW;
+            constexpr int cb = g & 1, ca = h & 1;
+            constexpr int slot = 2 * par + h;
+            constexpr int p0 = g < NGI ? (g * PPG < NP ? g * PPG : NP) : NP;
+            constexpr int p1 = g < NGI ? ((g + 1) * PPG < NP ? (g + 1) * PPG : NP) : NP;
+            static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
+            if constexpr (nt == 0) {
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) panel_fp8x8<slot>(af[ca][mt], a_sc, a8[mt]);
+            }
+            panel_fp8x8<slot>(bfr[cb][1], b_sc[nt], b8[nt]);
+            const bf16x8 b_hi = bfr[cb][0];
+            if constexpr (g + 1 < NG) {
+                constexpr int h1 = (g + 1) / G::NTW, nt1 = (g + 1) % G::NTW;
+                if constexpr (h1 != h) read_a(ab, h1, af[h1 & 1]);
+                read_b(ob, h1, nt1, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
+            } else {
+                wait_vm_barrier<G::LA>();   // stage s + 1 landed (only A(s+2) may be outstanding)
+                const char* abn = abufs + abuf_next * kPanelAStage;
+                const char* obn = obufs + ((s + 1) & 1) * G::OStage;
+                read_a(abn, 0, af[0]);   // the last group runs on af[1] (h = 1)
+                read_b(obn, 0, 0, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], b_hi, acc[mt][nt], 0, 0, 0);
+            if constexpr (par == 1 && h == 1) {
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[mt], b8[nt], acc[mt][nt], 0, 0, 0,
+                                                                                   a_e8, 0, b_e8[nt]);
+            }
+        });
+        abuf = abuf_next;
     };
     for (int s = 0; s < nsteps; s += 2) {
         stage(s, std::integral_constant<int, 0>{});
@@ -953,7 +1074,11 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (L8)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
+    if constexpr (L8 && ILV >= 2)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
+        panel_mainloop_pipe_lo8<NT, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
+                                            (int)(p.m / kPanelK), p.rexp, p.m / kPanelRows, 1,
+                                            (int)(p.m / kPanelRows), panel_a_exp(p.amax), acc);
+    else if constexpr (L8)
         panel_mainloop_lo8<NT, 1, ILV, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                             (int)(p.m / kPanelK), p.rexp, p.m / kPanelRows, 1,
                                             (int)(p.m / kPanelRows), panel_a_exp(p.amax), acc);
@@ -998,10 +1123,17 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
     const long long kc = p.w / p.kchunks;
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
-    if constexpr (L8 && NS == 2)   // the direction's lo piece on e4m3: scales from the chunk's tiles' max |D|
+    if constexpr (L8 && NS == 2 && ILV >= 2)   // the direction's lo piece on e4m3: scales from the chunk's tiles' max |D|
+        panel_mainloop_pipe_lo8<NT, 2, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
+                                            p.ldd, chunk * kc, (int)(kc / kPanelK),
+                                            p.dexp + (chunk * kc / kPanelRows) * p.k, 1, p.k,
+                                            (int)((chunk * kc % kPanelRows + kc + kPanelRows - 1) / kPanelRows),
+                                            panel_a_exp(p.amax), acc);
+    else if constexpr (L8 && NS == 2)
         panel_mainloop_lo8<NT, 2, ILV, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                             chunk * kc, (int)(kc / kPanelK), p.dexp + (chunk * kc / kPanelRows) * p.k,
-                                            1, p.k, (int)(kc / kPanelRows), panel_a_exp(p.amax), acc);
+                                            1, p.k, (int)((chunk * kc % kPanelRows + kc + kPanelRows - 1) / kPanelRows),
+                                            panel_a_exp(p.amax), acc);
     else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
         panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);

@@ -86,23 +86,27 @@ PanelLayout panel_layout(const bpgl_panel* c) {
 
 // ns: bf16 pieces of the direction (pass 1's epilogue writes it, pass 2 reads it): the
 // solver's d_split knob, 2 for the API products (bpgl_panel_mtm / _mm)
-// lo8 forms: 8 waves (WNX 0), mainloop ILV 0 / 1 (pass 1's default pipe form falls back to ILV 1)
-template <int NT, int NS>
-int panel_launch_lo8(bpgl_panel* c, int which) {
-    const bool i0 = c->interleave[which] == 0;
+// lo8 forms: 8 waves (WNX 0); mainloop ILV 0, 1 or 2 (the staggered form 3 falls back to 2)
+template <int NT, int NS, int ILV>
+int panel_launch_lo8_ilv(bpgl_panel* c, int which) {
     if (which == 0) {
-        if (i0) hipLaunchKernelGGL((k_panel_pass1<NT, 1, 0, NS, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
-                                   dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1, nullptr);
-        else hipLaunchKernelGGL((k_panel_pass1<NT, 1, 1, NS, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
-                                dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1, nullptr);
+        hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
+                           dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1, nullptr);
         LAUNCH_CHECK("k_panel_pass1");
     } else {
         const dim3 g((unsigned)((c->m / kPanelRows) * c->kchunks));
-        if (i0) hipLaunchKernelGGL((k_panel_pass2<NT, 0, 2, 0, 1>), g, dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1);
-        else hipLaunchKernelGGL((k_panel_pass2<NT, 1, 2, 0, 1>), g, dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1);
+        hipLaunchKernelGGL((k_panel_pass2<NT, ILV, 2, 0, 1>), g, dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1);
         LAUNCH_CHECK("k_panel_pass2");
     }
     return 0;
+}
+template <int NT, int NS>
+int panel_launch_lo8(bpgl_panel* c, int which) {
+    switch (c->interleave[which]) {
+        case 0: return panel_launch_lo8_ilv<NT, NS, 0>(c, which);
+        case 1: return panel_launch_lo8_ilv<NT, NS, 1>(c, which);
+        default: return panel_launch_lo8_ilv<NT, NS, 2>(c, which);
+    }
 }
 template <int NS>
 int panel_launch_lo8_ns(bpgl_panel* c, int which) {
