@@ -34,7 +34,7 @@ struct bpgl_panel {
     bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
     int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
     int waves[2] = {0, 0};        // waves along the RHS per pass: 0 = 2 (8 waves), 4 = 16 waves ("waves" knobs)
-    int dsplit = 2;               // bf16 pieces of the solver's direction (d_split knob)
+    int dsplit = 1;               // bf16 pieces of the solver's direction (d_split knob; 1 since round 4)
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)

@@ -327,19 +327,25 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * fragment reads one MFMA group ahead across the stage barrier (2, pass-1
  * default).
  * This one selects the solver's arithmetic (every choice is an exact line
- * search along the direction it takes): "d_split" 2 -- the direction enters
- * the A D pass as a hi + lo bf16 pair (~16-bit mantissa); 1 -- as its bf16
- * rounding alone (half the pass-2 MFMA work).  bpgl_panel_mtm / _mm always use
- * hi + lo operands.  bpgl_panel_get_tuning reads "interleave1", "interleave2",
- * "d_split". */
-/* "lo8" (mask; a reset must follow): the lo piece of the residual (bit 0, pass 1) and
- * of the direction (bit 1, pass 2) on block-scaled e4m3 MFMA
+ * search along the direction it takes): "d_split" 1 (default since ABI 200) --
+ * the direction enters the A D pass as its bf16 rounding alone (half the
+ * pass-2 MFMA work); 2 -- as a hi + lo bf16 pair (~16-bit mantissa).  Both
+ * converge to the same solution: after the reference's 1000 iterations at the
+ * configs[4] shape both are within 1.7-2.2e-5 of the fp64 oracle on x and 1e-11
+ * on the objective (the gradient pass, hi + lo always, sets the fixed point;
+ * profiles/r04/accuracy); short runs follow slightly different trajectories.
+ * bpgl_panel_mtm / _mm always use hi + lo operands.  bpgl_panel_get_tuning reads
+ * "interleave1", "interleave2", "d_split", "lo8", "r_refresh".
+ * "lo8" (mask; a reset must follow): the lo piece of the residual (bit 0, pass 1)
+ * and of the direction (bit 1, pass 2) on block-scaled e4m3 MFMA
  * (v_mfma_scale_f32_16x16x128_f8f6f4, twice the bf16 rate) against an e4m3 image of
- * A, the hi piece on bf16 as before: operands to ~2^-13 instead of ~2^-17.  With
- * bit 1 the product S no longer equals A D' exactly, so the incrementally updated
- * residual is recomputed exactly (R = A X - B from X's three bf16 pieces) every
- * "r_refresh" iterations (default 128; 0 = never; a multiple of 8).  lo8 passes use
- * the interleave 0 / 1 mainloops (2 and 3 fall back to 1) with 8 waves. */
+ * A, the hi piece on bf16 as before: operands to ~2^-13 instead of ~2^-17.  Opt-in,
+ * measured slower (the bf16 -> e4m3 conversions of the fragments cost more issue
+ * time than the matrix cores save) and, in pass 1, less accurate (x within 3.4e-4
+ * of the oracle instead of 2e-5).  With bit 1 the product S no longer equals A D'
+ * exactly, so the incrementally updated residual is recomputed exactly (R = A X - B
+ * from X's three bf16 pieces) every "r_refresh" iterations (default 128; 0 = never;
+ * a multiple of 8).  lo8 passes use the interleave 0 / 1 / 2 mainloops with 8 waves. */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_get_tuning(const bpgl_panel* ctx, const char* key, int64_t* value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);

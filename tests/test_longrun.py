@@ -63,17 +63,20 @@ def test_long_horizon_against_oracle(name):
 
 
 @pytest.mark.timeout(600)
-def test_panel_long_horizon_against_oracle():
+@pytest.mark.parametrize("d_split", [1, 2])
+def test_panel_long_horizon_against_oracle(d_split):
     """configs[4] (8192 x 65536 bf16 A, k = 128 right-hand sides), ITER_MAX = 1000 iterations of the
-    panel path (MFMA passes with hi + lo residual / direction), RHS 0 and 127 against the fp64 oracle on
-    the same bf16 A: x within 1e-3 relative l2 (the bound stated for this path, tests/test_panel.py), the
-    objective within 1e-5 relative."""
+    panel path (MFMA passes; the residual as hi + lo bf16, the direction as its bf16 rounding -- d_split
+    1, the default -- or as hi + lo), RHS 0, 42, 85 and 127 against the fp64 oracle on the same bf16 A:
+    x within 1e-4 relative l2 (measured 1.7-2.2e-5 for both forms, profiles/r04/accuracy: the
+    gradient pass sets the fixed point), the objective within 1e-5 relative (measured ~1e-11)."""
     from convex_optimization_amd.panel import PanelLasso
     path = os.path.join(GOLD, "longrun_configs4.npz")
     if not os.path.exists(path):
         pytest.skip(f"{path} not generated (tests/golden/make_longrun.py configs4)")
     fx = dict(np.load(path))
     m, n, k, IT = int(fx["m"]), int(fx["n"]), int(fx["k"]), int(fx["iters"])
+    assert len(fx["rhs"]) >= 4
     A = H.torch_A_bf16(m, n, "cuda:0")
     rows, cols = torch.from_numpy(fx["A_rows"]).cuda(), torch.from_numpy(fx["A_cols"]).cuda()
     assert np.array_equal(A[rows, cols].cpu().numpy(), fx["A_samples"]), "A differs from the fixture's"
@@ -84,6 +87,7 @@ def test_panel_long_horizon_against_oracle():
         assert hashlib.sha256(B[:, int(r)].cpu().numpy().tobytes()).hexdigest() == str(fx[f"b_sha256_{r}"])
         mu[int(r)] = float(fx[f"mu_{r}"])
     pl = PanelLasso(A, 1, nrhs=k, device=0)
+    pl.set_tuning("d_split", d_split)
     X = pl.run(B, mu, IT)["x"]
     for r in fx["rhs"]:
         r = int(r)
@@ -92,6 +96,6 @@ def test_panel_long_horizon_against_oracle():
         res = A64 @ x - B[:, r]
         f = 0.5 * float(res @ res) + float(mu[r]) * float(x.abs().sum())
         ef = abs(f - float(fx[f"objective_{r}"])) / float(fx[f"objective_{r}"])
-        print(f"configs4 RHS {r}, {IT} iterations: x rel l2 vs oracle {ex:.3e}, objective rel {ef:.3e}")
-        assert ex <= 1e-3, ex
+        print(f"configs4 d_split {d_split} RHS {r}, {IT} iterations: x rel l2 vs oracle {ex:.3e}, objective rel {ef:.3e}")
+        assert ex <= 1e-4, ex
         assert ef <= 1e-5, ef
