@@ -156,22 +156,33 @@ def test_panel_padded_layouts_are_bitwise_neutral(blocks, d_split):
 def test_panel_split_k_chunks_agree(kchunks):
     """Pass-2 column chunks only change the fp64 summation order of the fp32 chunk partials."""
     Ab, B, mu = instance(512, 2048, 32, seed=5)
-    base = PanelLasso(Ab, 1, nrhs=32, device=0).run(B, mu, 30)["x"]
+    # the hi + lo direction: with its bf16 rounding (d_split 1) a last-bit change of S can flip a
+    # rounding of D and move the short trajectory by more than the summation order itself does
+    b0 = PanelLasso(Ab, 1, nrhs=32, device=0)
+    b0.set_tuning("d_split", 2)
+    base = b0.run(B, mu, 30)["x"]
     pl = PanelLasso(Ab, 1, nrhs=32, device=0, kchunks=kchunks)
+    pl.set_tuning("d_split", 2)
     assert pl.kchunks == kchunks
     x = pl.run(B, mu, 30)["x"]
     assert np.linalg.norm(x - base) <= 1e-4 * np.linalg.norm(base)
 
 
-def test_panel_many_blocks_k128_matches_oracle():
+@pytest.mark.parametrize("d_split,fbound", [(2, 1e-5), (1, 1e-4)])
+def test_panel_many_blocks_k128_matches_oracle(d_split, fbound):
+    """4 feature blocks (cyclic order), k = 128, 40 iterations against the oracle: x within 1e-2; the
+    objective within 1e-5 for the hi + lo direction and 1e-4 for its bf16 rounding (the default), whose
+    short trajectory differs (measured 1.5e-5 here; both converge to the same solution,
+    tests/test_longrun.py)"""
     Ab, B, mu = instance(256, 2048, 128, seed=9)
     pl = PanelLasso(Ab, 4, nrhs=128, device=0)
+    pl.set_tuning("d_split", d_split)
     res = pl.run(B, mu, 40)
     for j in (0, 63, 127):
         ref = oracle.run(Ab, B[:, j], mu[j], 4, 40, nthreads=NT)["x"]
         assert np.linalg.norm(res["x"][:, j] - ref) <= 1e-2 * np.linalg.norm(ref)
         assert abs(objective(Ab, B[:, j], mu[j], res["x"][:, j]) - objective(Ab, B[:, j], mu[j], ref)) <= \
-            1e-5 * objective(Ab, B[:, j], mu[j], ref)
+            fbound * objective(Ab, B[:, j], mu[j], ref)
 
 
 def test_panel_argument_errors():
@@ -270,6 +281,7 @@ def test_panel_lo8_solver_matches_per_rhs_oracle(m, n, blocks, k, iters, lo8, rr
     1e-5 relative."""
     Ab, B, mu = instance(m, n, k, seed=7 + k)
     pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
+    pl.set_tuning("d_split", 2)   # lo8 bit 1 replaces the direction's lo piece: the hi + lo form
     pl.set_tuning("lo8", lo8)
     pl.set_tuning("r_refresh", rr)
     assert (pl.get_tuning("lo8"), pl.get_tuning("r_refresh")) == (lo8, rr)
@@ -294,6 +306,7 @@ def test_panel_lo8_graph_equals_eager():
     refresh runs between replays): bitwise equal iterates."""
     Ab, B, mu = instance(512, 1024, 128, seed=4)
     pl = PanelLasso(Ab, 1, nrhs=128, device=0)
+    pl.set_tuning("d_split", 2)
     pl.set_tuning("lo8", 3)
     pl.set_tuning("r_refresh", 16)
     a = pl.run(B, mu, 44, use_graph=True)["x"]
@@ -315,6 +328,7 @@ def test_panel_lo8_residual_refresh_pins_the_drift():
     a column chunk)."""
     Ab, B, mu = instance(512, 2048, 64, seed=17)
     pl = PanelLasso(Ab, 1, nrhs=64, device=0)
+    pl.set_tuning("d_split", 2)
     pl.solver_reset(B, mu)
     pl.solver_step(60)
     d_bf16 = _residual_drift(pl, Ab, B)
@@ -349,3 +363,27 @@ def test_panel_lo8_knob_errors():
     with pytest.raises(Exception):
         pl.solver_step(1)                    # a lo8 change needs a reset
     assert PanelLasso(Ab, 1, nrhs=16, device=0).kchunks == 4   # the automatic chunks fit lo8 (128 | w / kchunks)
+
+
+@pytest.mark.parametrize("d_split", [1, 2])
+@pytest.mark.parametrize("m,n,k", [(512, 2048, 32), (8192, 4096, 128), (4352, 1024, 16)])
+def test_panel_fused_tail_is_bitwise_equal(m, n, k, d_split):
+    """fuse_tail = 1 (k_panel_tail: the split-K reduce, the per-RHS line search and the update in one
+    launch, the blocks of a right-hand side meeting at its arrival counter) runs the same arithmetic in
+    the same order as k_panel_reduce + k_panel_update: bitwise equal iterates, error records and
+    residual; graph = eager; several blocks per RHS (m = 8192: 2) and a partial last block
+    (m = 4352)."""
+    Ab, B, mu = instance(m, n, k, seed=m + k)
+    pl = PanelLasso(Ab, 1, nrhs=k, device=0)
+    pl.set_tuning("d_split", d_split)
+    ref = pl.run(B, mu, 24, record=True)
+    R0 = pl.residual_device().cpu().numpy().copy()
+    pl.set_tuning("fuse_tail", 1)
+    assert pl.get_tuning("fuse_tail") == 1
+    for graph in (True, False):
+        got = pl.run(B, mu, 24, record=True, use_graph=graph)
+        np.testing.assert_array_equal(got["x"], ref["x"])
+        np.testing.assert_array_equal(got["err_iter"], ref["err_iter"])
+        assert got["iters"] == 24
+        pl.stream.synchronize()
+        np.testing.assert_array_equal(pl.residual_device().cpu().numpy(), R0)
