@@ -68,8 +68,7 @@ struct PanelState {
     double last_err;
     long long cur_mb;   // block of the iteration being finished (set by the line search)
     long long pending;  // one feature block: x += gamma D' of the last iteration not yet applied
-    long long fail;     // k_panel_tail: a block's wait for its RHS's other blocks timed out
-    long long pad[2];
+    long long pad[3];
 };
 
 struct PanelParams {
@@ -100,7 +99,6 @@ struct PanelParams {
     long long rec_len;
     PanelState* st;
     unsigned long long* cnt;   // [k] k_panel_reduce arrivals per RHS (monotone: launch q ends at q * groups)
-    unsigned long long* tcnt;  // [k + 1][16] k_panel_tail arrivals per RHS and per launch, one 128-B line each
     int wt;             // write-through store sites: 1 pass-1 epilogue (x, D'), 2 pass-2 slab, 4 S, 8 R
     // e4m3 lo products (the "lo8" knob, section "lo8" below)
     unsigned* amax;     // float bits of max |A| (k_panel_diag)
@@ -1426,234 +1424,6 @@ __global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p) {
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, true);
 }
 
-// ---------------------------------------------------------------------------
-// Fused iteration tail (one feature block, x updated here: the "fuse_tail" knob): k_panel_reduce,
-// its per-RHS line search and k_panel_update in one launch.  Block (rhs, q) of k x P, 1024 threads
-// (16 waves), owns rows [4096 q, 4096 q + 4096) of its RHS -- four 1024-row line-search groups, each
-// on 4 waves with k_panel_reduce's thread -> row map -- and columns [q w / P, (q + 1) w / P) of
-// its x (kTailThreads / kTailRows: one 1024-row group per block since round 4; 4096-row blocks of 1024
-// threads measured slower).  Phase 1: S = the chunks' fixed-order sum, the groups' r.s, s.s partials (the same
-// arithmetic and order as k_panel_reduce, so the same bits), S written; arrival at the RHS's
-// counter.  The P blocks of an RHS meet there (bounded wait: a timeout sets PanelState::fail and
-// the block commits nothing), then each runs the line search of panel_step_rhs (same order, same
-// gamma) and applies R += gamma S (R, S re-read from L2) with the hi / lo split and the exponent
-// table, and x += gamma D' on its columns.  The last block of the launch bumps t.  Per iteration
-// this saves S's and R's HBM round trip between the kernels and one kernel boundary.
-// ---------------------------------------------------------------------------
-constexpr int kTailThreads = 256;
-constexpr int kTailRows = 1024;        // rows per block: one line-search group
-constexpr unsigned kTailPolls = 1u << 22;
-__device__ __forceinline__ unsigned long long panel_ld_u64(const unsigned long long* q) {
-    return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <int DS>
-__global__ __launch_bounds__(kTailThreads) void k_panel_tail(PanelParams p, int P) {
-    const int rhs = blockIdx.x / P, q = blockIdx.x % P;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ng = (int)((p.m + kLspRows - 1) / kLspRows);
-    const long long km = (long long)p.k * p.m;
-    __shared__ double sr[16], sq[16], s3[3][kWaves];
-    __shared__ double bc[2];
-    __shared__ double lsr[kTailThreads][2];
-    __shared__ int ok;
-    // the norm partials of this RHS (pass-1 tiles), loaded first: panel_step_rhs's order (4 waves)
-    const int nb1 = (int)(p.w / kPanelRows);
-    double na = 0.0, nbv = 0.0, ne = 0.0;
-    if (tid < kThreads)
-        for (int t = tid; t < nb1; t += kThreads) {
-            const double* src = p.norms + ((long long)t * p.k + rhs) * 4;
-            na += src[0];
-            nbv += src[1];
-            ne = (src[2] > ne || src[2] != src[2]) ? src[2] : ne;
-        }
-    // phase 1: this thread's 4 rows of group grp (k_panel_reduce's map)
-    const int grp = q * (kTailRows / kLspRows) + (tid >> 8);
-    const long long i = (long long)grp * kLspRows + 4 * (tid & 255);
-    double rs = 0.0, ss = 0.0;
-    if (i < p.m) {
-        double sv[4] = {0.0, 0.0, 0.0, 0.0};
-        const double* rp = p.R + (long long)rhs * p.m + i;
-        const double2 r01 = *reinterpret_cast<const double2*>(rp);
-        const double2 r23 = *reinterpret_cast<const double2*>(rp + 2);
-        const float* src = p.Sslab + (long long)rhs * p.m + i;
-        auto add = [&](const float4& v) {
-            sv[0] += (double)v.x;
-            sv[1] += (double)v.y;
-            sv[2] += (double)v.z;
-            sv[3] += (double)v.w;
-        };
-        int c = 0;
-        for (; c + 8 <= p.kchunks; c += 8) {
-            float4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (c + u) * km);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) add(v[u]);
-        }
-        for (; c < p.kchunks; ++c) add(*reinterpret_cast<const float4*>(src + c * km));
-        const long long e = (long long)rhs * p.m + i;
-        *reinterpret_cast<double2*>(p.S + e) = make_double2(sv[0], sv[1]);
-        *reinterpret_cast<double2*>(p.S + e + 2) = make_double2(sv[2], sv[3]);
-        rs = fma(r01.x, sv[0], rs); rs = fma(r01.y, sv[1], rs);
-        rs = fma(r23.x, sv[2], rs); rs = fma(r23.y, sv[3], rs);
-        ss = fma(sv[0], sv[0], ss); ss = fma(sv[1], sv[1], ss);
-        ss = fma(sv[2], sv[2], ss); ss = fma(sv[3], sv[3], ss);
-    }
-    rs = wave_sum(rs);
-    ss = wave_sum(ss);
-    if (lane == 0) { sr[wave] = rs; sq[wave] = ss; }
-    if (tid < kThreads) {   // the norm sums, panel_step_rhs's fold
-        na = wave_sum(na);
-        nbv = wave_sum(nbv);
-        ne = wave_max(ne);
-        if (lane == 0) { s3[0][wave] = na; s3[1][wave] = nbv; s3[2][wave] = ne; }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        for (int g4 = 0; g4 < kTailRows / kLspRows; ++g4) {
-            const int g = q * (kTailRows / kLspRows) + g4;
-            if (g >= ng) break;
-            double* dst = p.lsp + ((long long)g * p.k + rhs) * 2;
-            panel_st_sc1(dst, ((sr[4 * g4] + sr[4 * g4 + 1]) + sr[4 * g4 + 2]) + sr[4 * g4 + 3]);
-            panel_st_sc1(dst + 1, ((sq[4 * g4] + sq[4 * g4 + 1]) + sq[4 * g4 + 2]) + sq[4 * g4 + 3]);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __atomic_thread_fence(__ATOMIC_RELEASE);
-        unsigned long long* cnt = p.tcnt + 16ll * rhs;
-        const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long target = (old / (unsigned long long)P + 1) * (unsigned long long)P;
-        unsigned n = kTailPolls;
-        int good = 1;
-        while (panel_ld_u64(cnt) < target) {
-            if (n-- == 0) { good = 0; break; }
-            __builtin_amdgcn_s_sleep(8);
-        }
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);
-        ok = good;
-    }
-    __syncthreads();
-    // the groups' line-search partials, one group per thread (all loads in flight at once), summed
-    // by thread 0 in group order -- panel_step_rhs's fold
-    double rt = 0.0, st = 0.0;
-    for (int g0 = 0; ok && g0 < ng; g0 += kTailThreads) {   // ok is block-uniform
-        const int gg = g0 + tid;
-        if (gg < ng) {
-            const double* src = p.lsp + ((long long)gg * p.k + rhs) * 2;
-            lsr[tid][0] = panel_ld_sc1(src);
-            lsr[tid][1] = panel_ld_sc1(src + 1);
-        }
-        __syncthreads();
-        if (tid == 0)
-            for (int u = 0; u < kTailThreads && g0 + u < ng; ++u) { rt += lsr[u][0]; st += lsr[u][1]; }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        double g = 0.0;
-        if (ok) {   // panel_step_rhs's line search, the same order
-            const double a = ((s3[0][0] + s3[0][1]) + s3[0][2]) + s3[0][3];
-            const double b = ((s3[1][0] + s3[1][1]) + s3[1][2]) + s3[1][3];
-            double e = s3[2][0];
-            for (int w4 = 1; w4 < kWaves; ++w4) e = (s3[2][w4] > e || s3[2][w4] != s3[2][w4]) ? s3[2][w4] : e;
-            const double r1 = rt + p.mu[rhs] * (a - b);
-            g = (st == 0.0) ? 0.0 : proj(-r1 / st, 0.0, 1.0);
-            if (q == 0) {
-                p.gamma[rhs] = g;
-                panel_st_sc1(p.err_rhs + rhs, e);
-            }
-        } else {
-            __hip_atomic_store(&p.st->fail, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        bc[0] = g;
-    }
-    __syncthreads();
-    if (ok) {
-        const double g = bc[0];
-        typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-        typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
-        // R += gamma S on this thread's rows (both from L2), split, exponent table
-        if (i < p.m) {
-            const long long e = (long long)rhs * p.m + i;
-            const long long re = (long long)rhs * p.ldr + i;
-            const double2 r01 = *reinterpret_cast<const double2*>(p.R + e);
-            const double2 r23 = *reinterpret_cast<const double2*>(p.R + e + 2);
-            const double2 s01 = *reinterpret_cast<const double2*>(p.S + e);
-            const double2 s23 = *reinterpret_cast<const double2*>(p.S + e + 2);
-            double r[4] = {r01.x + g * s01.x, r01.y + g * s01.y, r23.x + g * s23.x, r23.y + g * s23.y};
-            __bf16 hi[4], lo[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) split_bf16(r[u], hi[u], lo[u]);
-            *reinterpret_cast<double2*>(p.R + e) = make_double2(r[0], r[1]);
-            *reinterpret_cast<double2*>(p.R + e + 2) = make_double2(r[2], r[3]);
-            *reinterpret_cast<bf16x4v*>(p.Rh + re) = bf16x4v{hi[0], hi[1], hi[2], hi[3]};
-            *reinterpret_cast<bf16x4v*>(p.Rl + re) = bf16x4v{lo[0], lo[1], lo[2], lo[3]};
-            panel_put_rexp(p, (unsigned)(e / 4), r);
-        }
-        // x += gamma D' on this block's columns (k_panel_update's arithmetic)
-        const long long wq = ((p.w + P - 1) / P + 7) / 8 * 8, c0 = (long long)q * wq;
-        const long long c1 = c0 + wq < p.w ? c0 + wq : p.w;
-        // two 8-column units per trip, every load of a trip issued before its arithmetic
-        for (long long j0 = c0 + 8 * tid; j0 < c1; j0 += 16 * kTailThreads) {
-            bf16x8v dh[2], dl[2];
-            float4 xa[2], xb[2];
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                const long long j = j0 + (long long)v * 8 * kTailThreads;
-                if (j < c1) {
-                    const long long de = (long long)rhs * p.ldd + j;
-                    dh[v] = *reinterpret_cast<const bf16x8v*>(p.Dh + de);
-                    if constexpr (DS == 2) dl[v] = *reinterpret_cast<const bf16x8v*>(p.Dl + de);
-                    const float* xp = p.X + (long long)rhs * p.w + j;
-                    xa[v] = *reinterpret_cast<const float4*>(xp);
-                    xb[v] = *reinterpret_cast<const float4*>(xp + 4);
-                }
-            }
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                const long long j = j0 + (long long)v * 8 * kTailThreads;
-                if (j >= c1) continue;
-                float xs[8] = {xa[v].x, xa[v].y, xa[v].z, xa[v].w, xb[v].x, xb[v].y, xb[v].z, xb[v].w};
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    double dq = (double)(float)dh[v][u];
-                    if constexpr (DS == 2) dq += (double)(float)dl[v][u];
-                    xs[u] = (float)((double)xs[u] + g * dq);
-                }
-                float* xp = p.X + (long long)rhs * p.w + j;
-                *reinterpret_cast<float4*>(xp) = make_float4(xs[0], xs[1], xs[2], xs[3]);
-                *reinterpret_cast<float4*>(xp + 4) = make_float4(xs[4], xs[5], xs[6], xs[7]);
-            }
-        }
-    }
-    // the last block of the launch ends the iteration (the error record, t + 1)
-    __shared__ int last;
-    __syncthreads();
-    if (tid == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __atomic_thread_fence(__ATOMIC_RELEASE);
-        const unsigned long long nb = (unsigned long long)gridDim.x;
-        const unsigned long long old = __hip_atomic_fetch_add(p.tcnt + 16ll * p.k, 1ull, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-        last = ((old + 1) % nb) == 0;
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    }
-    __syncthreads();
-    if (last && tid < 64) {
-        double e = 0.0;
-        for (int j = tid; j < p.k; j += 64) {
-            const double v = panel_ld_sc1(p.err_rhs + j);
-            e = (v > e || v != v) ? v : e;
-        }
-        e = wave_max(e);
-        if (tid == 0) {
-            const long long t = p.st->t;
-            if (p.err_iter && t < p.rec_len) p.err_iter[t] = e;
-            p.st->last_err = e;
-            p.st->t = t + 1;
-            p.st->iters = t + 1;
-        }
-    }
-}
-
 // apply a pending x += gamma D' (one feature block) -- the end of every bpgl_panel_step, so the
 // iterates the caller reads are current; a no-op when nothing is pending
 template <int DS>
@@ -1835,7 +1605,6 @@ __global__ void k_panel_reset_state(PanelParams p) {
         p.st->last_err = 0.0;
         p.st->cur_mb = 0;
         p.st->pending = 0;
-        p.st->fail = 0;
     }
 }
 

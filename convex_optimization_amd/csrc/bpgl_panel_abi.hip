@@ -38,7 +38,6 @@ struct bpgl_panel {
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
-    int fuse_tail = 0;            // reduce + line search + update in one launch (k_panel_tail; "fuse_tail" knob)
     int lo8 = 0;                  // e4m3 lo products ("lo8" knob): bit 0 pass 1 (residual), bit 1 pass 2 (direction)
     int64_t r_period = 128;       // exact residual refresh every r_period iterations when pass 2 runs lo8 ("r_refresh")
     int64_t t_host = 0;           // iterations enqueued since the last reset
@@ -51,7 +50,7 @@ struct bpgl_panel {
 namespace {
 
 struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, tcnt, amax, rexp, dexp,
+    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, amax, rexp, dexp,
         X3, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
@@ -77,7 +76,6 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.gamma = k.take(8 * c->k);
     L.err_rhs = k.take(8 * c->k);
     L.cnt = k.take(8 * (int64_t)c->k);
-    L.tcnt = k.take(128 * ((int64_t)c->k + 1));   // the fused tail's counters, one 128-B line each
     L.amax = k.take(8);
     L.rexp = k.take(4 * (int64_t)c->k * (c->m / kPanelRows));
     L.dexp = k.take(4 * (c->w / kPanelRows) * (int64_t)c->k);
@@ -201,15 +199,6 @@ int panel_iteration(bpgl_panel* c, int64_t it) {
     if ((rc = panel_pass(c, 1))) return rc;
     panel_ev(c, it, 1, 1);
     panel_ev(c, it, 2, 0);
-    if (c->fuse_tail && c->nblock == 1 && !c->defer_x) {   // reduce, line search and update in one launch
-        const int P = (int)cdiv(c->m, kTailRows);
-        if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_tail<1>, dim3((unsigned)(c->k * P)), dim3(kTailThreads), 0,
-                                               c->stream, c->p, P);
-        else hipLaunchKernelGGL(k_panel_tail<2>, dim3((unsigned)(c->k * P)), dim3(kTailThreads), 0, c->stream, c->p, P);
-        LAUNCH_CHECK("k_panel_tail");
-        panel_ev(c, it, 2, 1);
-        return 0;
-    }
     if ((rc = panel_reduce(c, c->p.S, 1))) return rc;   // its last block per RHS runs the line search
     panel_ev(c, it, 2, 1);
     panel_ev(c, it, 4, 0);
@@ -387,7 +376,6 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.gamma = (double*)(s + L.gamma);
     p.err_rhs = (double*)(s + L.err_rhs);
     p.cnt = (unsigned long long*)(s + L.cnt);
-    p.tcnt = (unsigned long long*)(s + L.tcnt);
     p.amax = (unsigned*)(s + L.amax);
     p.rexp = (int*)(s + L.rexp);
     p.dexp = (int*)(s + L.dexp);
@@ -459,7 +447,6 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     p.err_iter = err_iter;
     p.rec_len = err_iter ? record_len : 0;
     HIP_TRY(hipMemsetAsync(p.cnt, 0, 8 * (int64_t)c->k, c->stream));   // arrival counters start at 0
-    HIP_TRY(hipMemsetAsync(p.tcnt, 0, 128 * ((int64_t)c->k + 1), c->stream));
     hipLaunchKernelGGL(k_panel_reset_state, dim3(1), dim3(64), 0, c->stream, c->p);
     LAUNCH_CHECK("k_panel_reset_state");
     if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
@@ -529,8 +516,6 @@ int bpgl_panel_status(bpgl_panel* c, int64_t* iters, double* last_err) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (iters) *iters = st.iters;
     if (last_err) *last_err = st.last_err;
-    if (st.fail) return fail(BPGL_E_EXCHANGE, "k_panel_tail: a block's wait for the other blocks of its right-hand "
-                                              "side timed out (not all blocks resident); the iterate is not valid");
     return 0;
 }
 
@@ -586,10 +571,6 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;
-    } else if (!strcmp(key, "fuse_tail")) {
-        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "fuse_tail must be 0 or 1");
-        c->fuse_tail = (int)value;
-        c->solver = false;   // the arrival counters of the two forms differ: a reset must follow
     } else if (!strcmp(key, "lo8")) {
         if (value < 0 || value > 3) return fail(BPGL_E_ARG, "lo8 is a mask: 1 pass 1 (residual), 2 pass 2 (direction)");
         if ((value & 2) && (c->w / c->kchunks) % (2 * kPanelK))
@@ -628,7 +609,6 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else if (!strcmp(key, "op_pad")) *value = c->op_pad;
     else if (!strcmp(key, "lo8")) *value = c->lo8;
-    else if (!strcmp(key, "fuse_tail")) *value = c->fuse_tail;
     else if (!strcmp(key, "r_refresh")) *value = c->r_period;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;

@@ -363,27 +363,3 @@ def test_panel_lo8_knob_errors():
     with pytest.raises(Exception):
         pl.solver_step(1)                    # a lo8 change needs a reset
     assert PanelLasso(Ab, 1, nrhs=16, device=0).kchunks == 4   # the automatic chunks fit lo8 (128 | w / kchunks)
-
-
-@pytest.mark.parametrize("d_split", [1, 2])
-@pytest.mark.parametrize("m,n,k", [(512, 2048, 32), (8192, 4096, 128), (4352, 1024, 16)])
-def test_panel_fused_tail_is_bitwise_equal(m, n, k, d_split):
-    """fuse_tail = 1 (k_panel_tail: the split-K reduce, the per-RHS line search and the update in one
-    launch, the blocks of a right-hand side meeting at its arrival counter) runs the same arithmetic in
-    the same order as k_panel_reduce + k_panel_update: bitwise equal iterates, error records and
-    residual; graph = eager; several blocks per RHS (m = 8192: 2) and a partial last block
-    (m = 4352)."""
-    Ab, B, mu = instance(m, n, k, seed=m + k)
-    pl = PanelLasso(Ab, 1, nrhs=k, device=0)
-    pl.set_tuning("d_split", d_split)
-    ref = pl.run(B, mu, 24, record=True)
-    R0 = pl.residual_device().cpu().numpy().copy()
-    pl.set_tuning("fuse_tail", 1)
-    assert pl.get_tuning("fuse_tail") == 1
-    for graph in (True, False):
-        got = pl.run(B, mu, 24, record=True, use_graph=graph)
-        np.testing.assert_array_equal(got["x"], ref["x"])
-        np.testing.assert_array_equal(got["err_iter"], ref["err_iter"])
-        assert got["iters"] == 24
-        pl.stream.synchronize()
-        np.testing.assert_array_equal(pl.residual_device().cpu().numpy(), R0)
