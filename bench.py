@@ -289,6 +289,16 @@ def build_problem(ctx, m, n_total, block, type_name, seed, force_comm=False, sha
     return gc, b, mu
 
 
+_T0 = time.time()
+
+
+def progress(msg):
+    """one line on stderr (rank 0): the phases of a long multi-leg run stay visible"""
+    if int(os.environ.get("RANK", "0")) == 0:
+        sys.stderr.write(f"# bench {time.time() - _T0:7.1f} s: {msg}\n")
+        sys.stderr.flush()
+
+
 def timed_window(ctx, sync, step, steps):
     """barrier + sync, exactly `steps` iterations, sync + barrier; max-over-ranks seconds."""
     ctx.barrier()
@@ -319,6 +329,7 @@ def measure(ctx, args, m, n_total):
     iterations; if a one-pass launch failed before the windows (every window then runs on the
     two-pass kernels), the solver is reset and the whole sequence measured once more."""
     import torch
+    progress(f"measure m={m} n={n_total} shard={args.shard} exchange_fp32={args.exchange_fp32}: building the instance")
     gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard)
     gc.set_tuning("fused", args.fused)
     gc.set_tuning("onepass", args.onepass)
@@ -339,12 +350,14 @@ def measure(ctx, args, m, n_total):
         torch.cuda.synchronize()
 
     for attempt in range(2):
+        progress(f"  attempt {attempt}: reset, {args.warmup} warm-up iterations")
         gc.solver_reset(b, mu, use_graph=True)
         op0 = gc.solver_stat("onepass")
         gc.solver_step(args.warmup)
         sync()
         # eager window: kernel averages (events on the solver stream) + clock ramp
         n_ev = max(args.steps, args.ramp)
+        progress(f"  eager window of {n_ev} iterations with kernel events")
         gc.set_kernel_timing(True)
         r0 = gc.solver_stat("refreshes")
         el_ev = timed_window(ctx, sync, gc.solver_step, n_ev)
@@ -360,6 +373,7 @@ def measure(ctx, args, m, n_total):
         # failed one-pass launch lost -- such a window did not do its K iterations, and a window
         # after a fallback runs the two-pass kernels: neither counts toward the median
         wins = []
+        progress(f"  {args.windows} graph windows of {args.steps} iterations")
         for _ in range(args.windows):
             r0 = gc.solver_stat("refreshes")
             rec0 = gc.solver_stat("fallbacks")
@@ -887,6 +901,7 @@ def main():
         },
     }
     if ctx.rank == 0 and not args.no_cpu:
+        progress("CPU baseline")
         note = "" if G == 1 else f" (rank 0's share of the {G}-GPU problem: {ml} x {w})"
         out["cpu_baseline"] = cpu_baseline(res["gc"], res["b"], res["mu"], args.cpu_seconds, cores, cpu_info, note)
         out["cpu_baseline"]["pool_configs0"] = pool

@@ -5,12 +5,10 @@
 set -o pipefail
 OUT=gpurun_out/r04_multi
 mkdir -p $OUT
-timeout -k 10 60 tools/_mfma_f8_probe > $OUT/mfma_f8_probe.txt 2>&1 &&
-timeout -k 10 60 tools/_cumask_probe > $OUT/cumask_probe.txt 2>&1 &&
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_ranks.py \
-    -k "8 or collective" > $OUT/pytest_rccl8.txt 2>&1 &&
+# rehearsals: every leg of the N > 1 line on CU partitions (short windows: the code path and the
+# JSON fields, not N-GPU rates -- the ranks share one GPU's HBM and RCCL runs over loopback sockets)
 for N in 8 2; do
   BPGL_BENCH_DEVICE=0 BPGL_BENCH_CU_PARTITION=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29700 + N)) bench.py --gpus $N \
-    > $OUT/n$N.json 2> $OUT/n$N.err || exit $?
+    --steps 32 --warmup 16 --ramp 32 --windows 3 --cpu-seconds 3 > $OUT/n$N.json 2> $OUT/n$N.err || exit $?
 done
