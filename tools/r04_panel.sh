@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/r04_panel
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_panel.py -k "mfma32 or gemms" \
+timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_panel.py tests/test_rowshard.py -k "mfma32 or gemms or in_kernel_fold" \
     > $OUT/pytest_panel.txt 2>&1
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for V in "-1 -1 0" "-1 -1 1" "-1 -1 0" "-1 -1 1"; do
