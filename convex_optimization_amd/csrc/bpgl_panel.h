@@ -1325,7 +1325,20 @@ __device__ __forceinline__ double panel_ld_sc1(const double* q) {
     return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(q),
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-template <bool LSP_SC1> __device__ void panel_step_rhs(const PanelParams& p, int rhs);
+template <bool LSP_SC1> __device__ void panel_step_rhs(const PanelParams& p, int rhs, double a, double b, double e);
+// this thread's share of the pass-1 norm partials of one RHS (tiles q = threadIdx.x, + kThreads, ...):
+// sum |Bx|, sum |x|, max err -- loaded by every k_panel_reduce block before its slab loads, so the last
+// block's line search does not wait for them
+__device__ __forceinline__ void panel_norm_share(const PanelParams& p, int rhs, double& a, double& b, double& e) {
+    const int nb1 = (int)(p.w / kPanelRows);
+    a = 0.0, b = 0.0, e = 0.0;
+    for (int q = threadIdx.x; q < nb1; q += kThreads) {
+        const double* src = p.norms + ((long long)q * p.k + rhs) * 4;
+        a += src[0];
+        b += src[1];
+        e = (src[2] > e || src[2] != src[2]) ? src[2] : e;
+    }
+}
 
 // S = sum over chunks (fp64, fixed order); line-search partials per RHS and
 // 1024-row group (mode 1), or plain output (mode 0, API).  grid = k x (m / 1024);
@@ -1336,6 +1349,8 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
     const int grp = blockIdx.x / p.k;
     const long long i = (long long)grp * kLspRows + 4 * threadIdx.x;
     double rs = 0.0, ss = 0.0;
+    double na = 0.0, nb = 0.0, ne = 0.0;
+    if (mode) panel_norm_share(p, rhs, na, nb, ne);
     if (i < p.m) {
         double s[4] = {0.0, 0.0, 0.0, 0.0};
         // the residual rows for the line-search partials, loaded up front (in flight with the chunk
@@ -1392,23 +1407,16 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
         last = ((old + 1) % ng) == 0;
     }
     __syncthreads();
-    if (last) panel_step_rhs<true>(p, rhs);
+    if (last) panel_step_rhs<true>(p, rhs, na, nb, ne);
 }
 
 // per-RHS line search (lasso.py:129-136): the pass-1 norm partials and the reduce's r.s / s.s
 // partials of one RHS folded in a fixed order -> gamma, err.  LSP_SC1: read the line-search
 // partials write-through (they were written by other blocks of the running launch).
+// a, b, e: this thread's share of the norm partials (panel_norm_share)
 template <bool LSP_SC1>
-__device__ void panel_step_rhs(const PanelParams& p, int rhs) {
+__device__ void panel_step_rhs(const PanelParams& p, int rhs, double a, double b, double e) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nb1 = (int)(p.w / kPanelRows);
-    double a = 0.0, b = 0.0, e = 0.0;
-    for (int q = threadIdx.x; q < nb1; q += kThreads) {
-        const double* src = p.norms + ((long long)q * p.k + rhs) * 4;
-        a += src[0];
-        b += src[1];
-        e = (src[2] > e || src[2] != src[2]) ? src[2] : e;
-    }
     __shared__ double s3[3][kWaves];
     a = wave_sum(a);
     b = wave_sum(b);
