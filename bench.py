@@ -158,8 +158,6 @@ def parse():
     ap.add_argument("--op-pad", type=int, default=0,
                     help="panel path: bf16 elements appended to each RHS row of the operand images (multiple of 64)")
     ap.add_argument("--lda-pad", type=int, default=0, help="panel path: columns appended to each row of bf16 A")
-    ap.add_argument("--mfma32", type=int, default=-1, choices=[-1, 0, 1],
-                    help="panel path: pass 1 on 32x32x16 MFMAs (1) or 16x16x32 (0); -1: library default")
     ap.add_argument("--lo8", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                     help="panel path: e4m3 lo products, bit 0 pass 1 (residual), bit 1 pass 2 (direction); "
                          "-1: library default")
@@ -676,8 +674,6 @@ def main_panel(args):
         pl.set_tuning("write_through", args.write_through)
     if args.lo8 >= 0:
         pl.set_tuning("lo8", args.lo8)
-    if args.mfma32 >= 0:
-        pl.set_tuning("mfma32", args.mfma32)
     if args.r_refresh >= 0:
         pl.set_tuning("r_refresh", args.r_refresh)
     for q in (1, 2):
@@ -734,7 +730,6 @@ def main_panel(args):
             "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
             "defer_x": pl.get_tuning("defer_x"), "op_pad": pl.get_tuning("op_pad"), "lda_pad": args.lda_pad,
             "lo8": pl.get_tuning("lo8"), "r_refresh": pl.get_tuning("r_refresh"), "refreshes": pl.stat("refreshes"),
-            "mfma32": pl.get_tuning("mfma32"),
             "interleave12": [pl.get_tuning("interleave1"), pl.get_tuning("interleave2")],
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,

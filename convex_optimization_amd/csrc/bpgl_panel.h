@@ -906,161 +906,6 @@ __device__ __forceinline__ void panel_mainloop_pipe_lo8(char* smem, const __bf16
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
-// ---------------------------------------------------------------------------
-// Pass 1 on 32 x 32 x 16 bf16 MFMAs (the "mfma32" knob, k = 128).  Round 3 measured the 32 x 32 shape
-// holding a higher clock than 16 x 16 x 32 at the same MAC count on this power-limited pass (+5 %, pass 2
-// +16 %; profiles/r03/panel_clock_m32) in a build whose dependent MFMAs ran back to back.  Here a wave
-// owns 2 x 2 tiles of 32 A-columns x 32 RHS (64 x 64 as before) and each 16-K step issues the hi and lo
-// MFMAs of the four tiles in turn, so an accumulator's dependent MFMAs are four apart.  Fragments
-// (lane l, s = 16-K step of the 64-K stage): A^T column j0 + (l & 31), K rows 16 s + 8 (l >> 5) + 0..7,
-// two transposing ds_read_b64_tr_b16 per fragment from an A image whose 16-B chunk c of row r sits at
-// c ^ 4 (r & 3) (the 16 (row, chunk) pairs a 32-lane read phase touches land on 16 distinct bank
-// groups); R column (RHS) l & 31 of the N tile, K 16 s + 8 (l >> 5) + 0..7 from the usual operand image.
-// After the mainloop the accumulators are repacked through LDS into the 16 x 16 C layout, so the
-// epilogue is the common one.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int swz512_32(int r, int c) { return c ^ (4 * (r & 3)); }
-template <int NT>
-__device__ __forceinline__ void panel_a1_piece32(int q, const __bf16* __restrict__ A, long long lda, long long ks,
-                                                 long long col0, char* abuf, int wave, int lane) {
-    using G = PanelGeo<NT, 2, 0>;
-    const int pc = q * G::NW + wave;
-    const int row = pc * 2 + (lane >> 5);
-    const int c = swz512_32(row, lane & 31);
-    glds16a(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
-}
-__device__ __forceinline__ bf16x8 panel_afrag1_32(const char* abuf, int j0, int s, int lane) {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int c = ((j0 + 16 * (g & 1)) >> 3) + (p >> 1);
-    const int r0 = 16 * s + 8 * (g >> 1) + q;
-    const int r1 = r0 + 4;
-    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(abuf + r0 * 512 + 16 * swz512_32(r0, c) + 8 * (p & 1)));
-    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(abuf + r1 * 512 + 16 * swz512_32(r1, c) + 8 * (p & 1)));
-    typedef short s16x8 __attribute__((ext_vector_type(8)));
-    const s16x8 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, v);
-}
-__device__ __forceinline__ bf16x8 panel_bfrag32(const char* obuf, int rr, int s, int lane) {
-    return *reinterpret_cast<const bf16x8*>(obuf + rr * 128 + 16 * swz128(rr, 2 * s + (lane >> 5)));
-}
-template <int NT, int ILV>
-__device__ __forceinline__ void panel_mainloop32_p1(char* smem, const __bf16* __restrict__ A, long long lda,
-                                                    long long a_col0, const __bf16* __restrict__ bh,
-                                                    const __bf16* __restrict__ bl, long long ldb, int nsteps,
-                                                    f32x16 (&acc)[2][2]) {
-    using G = PanelGeo<NT, 2, 0>;
-    static_assert(G::NTW == 4 && G::NW == 8, "the 32 x 32 form is built for k = 128 with 8 waves");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    char* abufs = smem;
-    char* obufs = smem + kPanelNA * kPanelAStage;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-    auto piece = [&](int i, int so, int bo, int sa, int ba) {
-        if (i < G::LO) {
-            panel_op_piece<NT, 2, 0>(i, bh, bl, ldb, (long long)so * kPanelK, obufs + bo * G::OStage, wave, lane);
-        } else {
-            panel_a1_piece32<NT>(i - G::LO, A, lda, (long long)sa * kPanelK, a_col0, abufs + ba * kPanelAStage, wave,
-                                 lane);
-        }
-    };
-    constexpr int NP = G::LO + G::LA;
-    constexpr int NG = 4;                            // MFMA groups per stage: the 16-K steps
-    constexpr int PPG = (NP + NG - 1) / NG;
-#pragma unroll
-    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
-#pragma unroll
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
-#pragma unroll
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
-    int abuf = 0;
-    for (int s = 0; s < nsteps; ++s) {
-        wait_vm_barrier<G::LA>();
-        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;
-        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
-        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;
-        if (!ILV) {
-#pragma unroll
-            for (int i = 0; i < NP; ++i) piece(i, so, bo, sa, ba);
-        }
-        const char* ab = abufs + abuf * kPanelAStage;
-        const char* ob = obufs + (s & 1) * G::OStage;
-        static_for<0, NG>([&](auto kc) {
-            constexpr int ks = decltype(kc)::value;
-            constexpr int p0 = ks * PPG < NP ? ks * PPG : NP;
-            constexpr int p1 = (ks + 1) * PPG < NP ? (ks + 1) * PPG : NP;
-            if constexpr (ILV) {
-                static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
-            }
-            bf16x8 af[2], bhi[2], blo[2];
-#pragma unroll
-            for (int mh = 0; mh < 2; ++mh) af[mh] = panel_afrag1_32(ab, wm * 64 + mh * 32, ks, lane);
-#pragma unroll
-            for (int nh = 0; nh < 2; ++nh) {
-                const int rr = wn * 64 + nh * 32 + (lane & 31);
-                bhi[nh] = panel_bfrag32(ob, rr, ks, lane);
-                blo[nh] = panel_bfrag32(ob, G::K + rr, ks, lane);
-            }
-#pragma unroll
-            for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-                for (int mh = 0; mh < 2; ++mh)
-                    acc[mh][nh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mh], bhi[nh], acc[mh][nh], 0, 0, 0);
-#pragma unroll
-            for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-                for (int mh = 0; mh < 2; ++mh)
-                    acc[mh][nh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mh], blo[nh], acc[mh][nh], 0, 0, 0);
-            if constexpr (ILV) {
-                if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
-                __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
-            }
-        });
-        abuf = abuf == 2 ? 0 : abuf + 1;
-    }
-    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the repack
-}
-// 32 x 32 accumulators (C: column (RHS) l & 31, row (A column) (reg & 3) + 8 (reg >> 2) + 4 (l >> 5))
-// -> the 16 x 16 C layout of the common epilogue (row (l >> 4) * 4 + r, column l & 15), through an
-// LDS image [128 RHS][257 fp32] (odd pitch: conflict-free columns)
-constexpr int kRepackPitch = 257;
-constexpr int kRepackBytes = 128 * kRepackPitch * 4;
-template <int NTW>
-__device__ __forceinline__ void panel_repack32(const f32x16 (&acc32)[2][2], f32x4 (&acc)[4][NTW], char* smem, int wm,
-                                               int wn, int lane) {
-    float* img = reinterpret_cast<float*>(smem);
-    __syncthreads();
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int col = wm * 64 + mh * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-                const int rhs = wn * 64 + nh * 32 + (lane & 31);
-                img[rhs * kRepackPitch + col] = acc32[mh][nh][reg];
-            }
-    __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
-                const int col = wm * 64 + mt * 16 + (lane >> 4) * 4 + r;
-                acc[mt][nt][r] = img[rhs * kRepackPitch + col];
-            }
-    __syncthreads();
-}
-
 // Write-through (sc1) stores for the bulk outputs a kernel hands to the next launch (split-K
 // slab, D', x, S, R and its split): the lines do not sit dirty in the XCD L2s at the kernel
 // boundary, whose cost grows by ~1 us per 6 MB left dirty (MI355X_MICROARCH.md, "boundary").
@@ -1219,7 +1064,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
 // epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
 // per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI, int ILV, int DS, int WNX, int L8 = 0, int M32 = 0>
+template <int NT, int EPI, int ILV, int DS, int WNX, int L8 = 0>
 __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
                                                                          double* __restrict__ Gout) {
     using G = PanelGeo<NT, 2, WNX>;
@@ -1229,15 +1074,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (M32 && NT == 8 && WNX == 0) {   // 32 x 32 x 16 MFMAs, repacked for the common epilogue
-        f32x16 acc32[2][2];
-        panel_mainloop32_p1<NT, ILV>(smem, p.A, p.lda, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr,
-                                     (int)(p.m / kPanelK), acc32);
-        panel_repack32<G::NTW>(acc32, acc, smem, wm, wn, threadIdx.x & 63);
-        static_assert(kRepackBytes + 4 * 128 * 4 * 8 <= G::Smem || NT != 8, "LDS budget of the repack");
-        panel_pass1_epilogue<G::NTW, EPI, DS>(p, mb, c0, wm, wn, G::T, acc, smem + kRepackBytes, Gout);
-        return;
-    } else if constexpr (L8 && ILV >= 2)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
+    if constexpr (L8 && ILV >= 2)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
         panel_mainloop_pipe_lo8<NT, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                             (int)(p.m / kPanelK), p.rexp, p.m / kPanelRows, 1,
                                             (int)(p.m / kPanelRows), panel_a_exp(p.amax), acc);

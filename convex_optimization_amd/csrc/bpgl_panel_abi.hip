@@ -38,7 +38,6 @@ struct bpgl_panel {
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
-    int mfma32 = 0;               // pass 1 on 32 x 32 x 16 MFMAs (k = 128; "mfma32" knob)
     int lo8 = 0;                  // e4m3 lo products ("lo8" knob): bit 0 pass 1 (residual), bit 1 pass 2 (direction)
     int64_t r_period = 128;       // exact residual refresh every r_period iterations when pass 2 runs lo8 ("r_refresh")
     int64_t t_host = 0;           // iterations enqueued since the last reset
@@ -168,25 +167,8 @@ int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mod
     return ns == 1 ? panel_launch_ns<1>(c, which, fixed_block, out, mode)
                    : panel_launch_ns<2>(c, which, fixed_block, out, mode);
 }
-// pass 1 on 32 x 32 x 16 MFMAs (k = 128, 8 waves): EPI 1 (solver) or 0 (G for the API)
-template <int EPI>
-int panel_pass1_m32(bpgl_panel* c, int fixed_block, double* out) {
-    const dim3 g((unsigned)(c->w / kPanelRows)), b(PanelGeo<8, 2, 0>::T);
-    const bool i0 = c->interleave[0] == 0;
-    if (EPI == 0 || c->dsplit == 2) {
-        if (i0) hipLaunchKernelGGL((k_panel_pass1<8, EPI, 0, 2, 0, 0, 1>), g, b, 0, c->stream, c->p, fixed_block, out);
-        else hipLaunchKernelGGL((k_panel_pass1<8, EPI, 1, 2, 0, 0, 1>), g, b, 0, c->stream, c->p, fixed_block, out);
-    } else {
-        if (i0) hipLaunchKernelGGL((k_panel_pass1<8, EPI, 0, 1, 0, 0, 1>), g, b, 0, c->stream, c->p, fixed_block, out);
-        else hipLaunchKernelGGL((k_panel_pass1<8, EPI, 1, 1, 0, 0, 1>), g, b, 0, c->stream, c->p, fixed_block, out);
-    }
-    LAUNCH_CHECK("k_panel_pass1");
-    return 0;
-}
-bool panel_m32(const bpgl_panel* c) { return c->mfma32 && c->k == 128 && c->waves[0] == 0 && !(c->lo8 & 1); }
 // a solver pass: the lo8 form when the knob selects it for this pass (pass 2 needs the hi + lo direction)
 int panel_pass(bpgl_panel* c, int which) {
-    if (which == 0 && panel_m32(c)) return panel_pass1_m32<1>(c, -1, nullptr);
     const bool l8 = which == 0 ? (c->lo8 & 1) != 0 : ((c->lo8 & 2) != 0 && c->dsplit == 2);
     if (l8) return c->dsplit == 1 ? panel_launch_lo8_ns<1>(c, which) : panel_launch_lo8_ns<2>(c, which);
     return panel_launch(c, which, -1, nullptr, 1, c->dsplit);
@@ -428,7 +410,6 @@ int bpgl_panel_mtm(bpgl_panel* c, int32_t block, const double* R, double* G) {
     HIP_TRY(hipSetDevice(c->device));
     if ((rc = panel_split(c, R, c->m, c->ldr(), c->p.Rh, c->p.Rl, 1.0, nullptr))) return rc;
     c->solver = false;   // Rh/Rl now hold the caller's operand
-    if (panel_m32(c)) return panel_pass1_m32<0>(c, block, G);
     return panel_launch(c, 0, block, G, 0, 2);
 }
 
@@ -590,9 +571,6 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;
-    } else if (!strcmp(key, "mfma32")) {
-        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "mfma32 must be 0 or 1");
-        c->mfma32 = (int)value;
     } else if (!strcmp(key, "lo8")) {
         if (value < 0 || value > 3) return fail(BPGL_E_ARG, "lo8 is a mask: 1 pass 1 (residual), 2 pass 2 (direction)");
         if ((value & 2) && (c->w / c->kchunks) % (2 * kPanelK))
@@ -631,7 +609,6 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else if (!strcmp(key, "op_pad")) *value = c->op_pad;
     else if (!strcmp(key, "lo8")) *value = c->lo8;
-    else if (!strcmp(key, "mfma32")) *value = c->mfma32;
     else if (!strcmp(key, "r_refresh")) *value = c->r_period;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;

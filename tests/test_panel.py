@@ -363,26 +363,3 @@ def test_panel_lo8_knob_errors():
     with pytest.raises(Exception):
         pl.solver_step(1)                    # a lo8 change needs a reset
     assert PanelLasso(Ab, 1, nrhs=16, device=0).kchunks == 4   # the automatic chunks fit lo8 (128 | w / kchunks)
-
-
-def test_panel_mfma32_pass1_matches():
-    """mfma32 = 1 (pass 1 on 32 x 32 x 16 MFMAs, k = 128, repacked into the common epilogue): the A^T R
-    product within 1e-4 (max-norm, relative) of fp64 on the same bf16 A, and the solver within the path's
-    tolerance of the oracle (the 16 x 16 form differs only in fp32 summation order)"""
-    m, n, k = 512, 2048, 128
-    Ab, B, mu = instance(m, n, k, seed=31)
-    pl = PanelLasso(Ab, 1, nrhs=k, device=0)
-    pl.set_tuning("mfma32", 1)
-    assert pl.get_tuning("mfma32") == 1
-    R = np.random.RandomState(4).randn(m, k)
-    G = pl.mat_tMulMat(R, 0).cpu().numpy()
-    ref = Ab.T @ R
-    assert np.abs(G - ref).max() <= 1e-4 * np.abs(ref).max(), np.abs(G - ref).max() / np.abs(ref).max()
-    for ds in (2, 1):
-        pl.set_tuning("d_split", ds)
-        X = pl.run(B, mu, 60)["x"]
-        for j in (0, 77, 127):
-            xo = oracle.run(Ab, B[:, j], mu[j], 1, 60, nthreads=NT)["x"]
-            assert np.linalg.norm(X[:, j] - xo) <= 1e-2 * np.linalg.norm(xo)
-            f_dev, f_ref = objective(Ab, B[:, j], mu[j], X[:, j]), objective(Ab, B[:, j], mu[j], xo)
-            assert abs(f_dev - f_ref) <= 1e-4 * f_ref
