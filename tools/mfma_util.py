@@ -41,7 +41,7 @@ def durations(d):
 def main():
     root = sys.argv[1]
     dur = durations(os.path.join(root, "trace"))
-    res = {"source": "tools/panel_mfma_pmc.sh (rocprofv3 --pmc, one pass per k) + kernel trace of bench.py --config 4",
+    res = {"source": "tools/profile_r04.sh (rocprofv3 --pmc, one pass per k; round 4, d_split 1) + kernel trace of bench.py --config 4",
            "simds": SIMDS, "peak_clock_hz": PEAK_HZ}
     for kdir in sorted(glob.glob(os.path.join(root, "k*"))):
         k = os.path.basename(kdir)
