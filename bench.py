@@ -164,6 +164,11 @@ def parse():
     ap.add_argument("--r-refresh", type=int, default=-1,
                     help="panel path with lo8 in pass 2: exact residual refresh period (multiple of 8; 0 never; "
                          "-1: library default)")
+    ap.add_argument("--carry-g", type=int, default=-1, choices=[-1, 0, 1],
+                    help="panel path, one block: carry G += gamma A^T S (one bf16 product in pass 1) between exact "
+                         "hi+lo gradients (1); -1: library default")
+    ap.add_argument("--g-refresh", type=int, default=-1,
+                    help="panel path with carry_g: exact gradient period (multiple of 8); -1: library default")
     ap.add_argument("--defer-x", type=int, default=-1, choices=[-1, 0, 1],
                     help="panel path, one block: apply x += gamma D in the next pass-1 epilogue (1) or in the "
                          "update kernel (0); -1: library default")
@@ -676,10 +681,15 @@ def main_panel(args):
         pl.set_tuning("lo8", args.lo8)
     if args.r_refresh >= 0:
         pl.set_tuning("r_refresh", args.r_refresh)
+    if args.carry_g >= 0:
+        pl.set_tuning("carry_g", args.carry_g)
+    if args.g_refresh >= 0:
+        pl.set_tuning("g_refresh", args.g_refresh)
     for q in (1, 2):
         if getattr(args, f"waves{q}") >= 0:
             pl.set_tuning(f"waves{q}", getattr(args, f"waves{q}"))
     d_split = pl.get_tuning("d_split")
+    carry, g_period = pl.get_tuning("carry_g"), pl.get_tuning("g_refresh")
     del A
     Ab = pl.A_bf16.float()
     B = (Ab @ Xt + 0.01 * torch.randn(m, k, device="cuda", generator=g)).double()
@@ -709,8 +719,10 @@ def main_panel(args):
     fill_bytes = panel_fill_bytes(m, w, k, 1 if dom == "pass1_mfma" else 2, d_split)
     achieved = pb / (kms[dom] * 1e-3) / 1e9
     # MFMA work of the dominant pass: the residual always enters as hi + lo, the direction
-    # as hi + lo (d_split 2) or hi alone (d_split 1)
-    flops = 2 * m * w * k * (2 if dom == "pass1_mfma" else d_split)
+    # as hi + lo (d_split 2) or hi alone (d_split 1); with carry_g pass 1 runs the bf16 S product and,
+    # every g_refresh iterations, the hi + lo residual products
+    p1_products = (1 + 2 / g_period) if carry else 2
+    flops = 2 * m * w * k * (p1_products if dom == "pass1_mfma" else d_split)
     tflops = flops / (kms[dom] * 1e-3) / 1e12
     iters_s = args.steps / el_graph
     alg_iter = 2 * m * w * 2 + 4 * k * 5 * (w + m)          # SURVEY.md 8d (c5: 2.336e9 B -> 3425 it/s)
@@ -721,7 +733,8 @@ def main_panel(args):
         "ms_per_step": el_graph / args.steps * 1e3, "higher_is_better": True, "scaling": "none",
         "vs_baseline": None,
         "dtype": "bf16 (A) x hi+lo bf16 residual x " + ("hi+lo bf16" if d_split == 2 else "bf16") +
-                 " direction, fp32 MFMA accumulate, fp64 reduce",
+                 " direction, fp32 MFMA accumulate, fp64 reduce" +
+                 (f"; gradient carried in fp32 (G += gamma A^T bf16 S), exact every {g_period}" if carry else ""),
         "data": "synthetic (A ~ N(0,1) rows unit-norm, bf16 in HBM; X_true density 0.4; B = A X_true + 0.01 E)",
         "config": {
             "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
@@ -730,6 +743,7 @@ def main_panel(args):
             "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
             "defer_x": pl.get_tuning("defer_x"), "op_pad": pl.get_tuning("op_pad"), "lda_pad": args.lda_pad,
             "lo8": pl.get_tuning("lo8"), "r_refresh": pl.get_tuning("r_refresh"), "refreshes": pl.stat("refreshes"),
+            "carry_g": carry, "g_refresh": g_period,
             "interleave12": [pl.get_tuning("interleave1"), pl.get_tuning("interleave2")],
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,

@@ -100,6 +100,9 @@ struct PanelParams {
     PanelState* st;
     unsigned long long* cnt;   // [k] k_panel_reduce arrivals per RHS (monotone: launch q ends at q * groups)
     int wt;             // write-through store sites: 1 pass-1 epilogue (x, D'), 2 pass-2 slab, 4 S, 8 R
+    // carried gradient (the "carry_g" knob, one feature block): G_t = G_{t-1} + gamma_{t-1} A^T S_{t-1}
+    float* Gc;          // [k][w]   the carried gradient (fp32)
+    __bf16* Sh;         // [k][ldr] bf16 image of S (k_panel_reduce), pass 1's operand in a carried iteration
     // e4m3 lo products (the "lo8" knob, section "lo8" below)
     unsigned* amax;     // float bits of max |A| (k_panel_diag)
     int* rexp;          // [k][m / 256]   frexp exponent of max |R| per 256-row group (update, reset, refresh)
@@ -953,7 +956,9 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 // [k][w] fp64 (API); EPI 1 is the fused shrink -- the direction D' in DS bf16 pieces, the norms
 // per RHS and block.  The wave owns output rows c0 + 64 wm .. (A columns) x RHS tiles wn * NTW ..;
 // T threads per block; smem holds at least 4 * k * 3 doubles and is free (after a barrier).
-template <int NTW, int EPI, int DS>
+// GM (carried gradient, one feature block): 0 -- g is the product (A^T R); 1 -- the same, also stored as
+// the carried G; 2 -- the product is U = A^T S_{t-1} and g = G + gamma_{t-1} U, stored back
+template <int NTW, int EPI, int DS, int GM = 0>
 __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int mb, long long c0, int wm, int wn,
                                                      int T, f32x4 (&acc)[4][NTW], char* smem,
                                                      double* __restrict__ Gout) {
@@ -983,6 +988,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
         const double mu = p.mu[rhs];
         const double gprev = fx ? p.gamma[rhs] : 0.0;
+        const double gcar = GM == 2 ? p.gamma[rhs] : 0.0;   // gamma_{t-1}: G_t = G_{t-1} + gamma_{t-1} U
         double sbx = 0.0, sx = 0.0, err = 0.0, dmax = 0.0;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
@@ -1004,9 +1010,16 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                        make_float4(xs[0], xs[1], xs[2], xs[3]));
             }
             __bf16 dh[4], dl[4];
+            float gs[4];
+            if constexpr (GM == 2) {
+                const float4 g4 = *reinterpret_cast<const float4*>(p.Gc + (long long)rhs * p.w + j);
+                gs[0] = g4.x; gs[1] = g4.y; gs[2] = g4.z; gs[3] = g4.w;
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double g = (double)acc[mt][nt][r];
+                double g = (double)acc[mt][nt][r];
+                if constexpr (GM == 2) g = (double)gs[r] + gcar * g;
+                if constexpr (GM != 0) gs[r] = (float)g;
                 const double x = (double)xs[r];
                 const long long kx = (long long)mb * p.w + j + r;
                 const double bx = p.rec[kx] * soft_thr(p.diag[kx] * x - g, mu);
@@ -1024,6 +1037,8 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 const double e = fabs(g - proj(g - x, -mu, mu));
                 err = (e > err || e != e) ? e : err;
             }
+            if constexpr (GM != 0)
+                *reinterpret_cast<float4*>(p.Gc + (long long)rhs * p.w + j) = make_float4(gs[0], gs[1], gs[2], gs[3]);
             wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
             if constexpr (DS == 2)
                 wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
@@ -1064,7 +1079,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
 // epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
 // per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI, int ILV, int DS, int WNX, int L8 = 0>
+template <int NT, int EPI, int ILV, int DS, int WNX, int L8 = 0, int GM = 0>
 __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
                                                                          double* __restrict__ Gout) {
     using G = PanelGeo<NT, 2, WNX>;
@@ -1074,7 +1089,16 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (L8 && ILV >= 2)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
+    if constexpr (GM == 2) {   // carried iteration: U = A^T S_{t-1} from the bf16 image of S alone
+        if constexpr (ILV >= 2)
+            panel_mainloop_pipe<NT, 1, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
+                                               (int)(p.m / kPanelK), acc);
+        else
+            panel_mainloop<NT, 1, ILV, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
+                                               (int)(p.m / kPanelK), acc);
+        panel_pass1_epilogue<G::NTW, EPI, DS, 2>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
+        return;
+    } else if constexpr (L8 && ILV >= 2)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
         panel_mainloop_pipe_lo8<NT, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                             (int)(p.m / kPanelK), p.rexp, p.m / kPanelRows, 1,
                                             (int)(p.m / kPanelRows), panel_a_exp(p.amax), acc);
@@ -1092,7 +1116,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
         panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                            (int)(p.m / kPanelK), acc);
 
-    panel_pass1_epilogue<G::NTW, EPI, DS>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
+    panel_pass1_epilogue<G::NTW, EPI, DS, GM>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
 }
 
 // ---------------------------------------------------------------------------
@@ -1218,6 +1242,11 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
         const long long e = (long long)rhs * p.m + i;
         wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e, make_double2(s[0], s[1]));
         wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e + 2, make_double2(s[2], s[3]));
+        if (mode && p.Sh) {   // the carried gradient's operand for the next pass 1
+            typedef __bf16 bf16x4s __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4s*>(p.Sh + (long long)rhs * p.ldr + i) =
+                bf16x4s{to_bf16((float)s[0]), to_bf16((float)s[1]), to_bf16((float)s[2]), to_bf16((float)s[3])};
+        }
         if (mode) {
             rs = fma(r01.x, s[0], rs); rs = fma(r01.y, s[1], rs);
             rs = fma(r23.x, s[2], rs); rs = fma(r23.y, s[3], rs);

@@ -38,6 +38,10 @@ struct bpgl_panel {
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
+    int carry_g = 0;              // carried gradient, one feature block ("carry_g" knob)
+    int64_t g_period = 64;        // exact gradient every g_period iterations ("g_refresh" knob)
+    int gm_cur = 0;               // pass-1 form of the launch being enqueued: 0 plain, 1 exact + store G, 2 carried
+    hipGraphExec_t gexec_ref = nullptr;   // carry_g: a graph whose first iteration is the exact-gradient one
     int lo8 = 0;                  // e4m3 lo products ("lo8" knob): bit 0 pass 1 (residual), bit 1 pass 2 (direction)
     int64_t r_period = 128;       // exact residual refresh every r_period iterations when pass 2 runs lo8 ("r_refresh")
     int64_t t_host = 0;           // iterations enqueued since the last reset
@@ -51,7 +55,7 @@ namespace {
 
 struct PanelLayout {
     int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, amax, rexp, dexp,
-        X3, total;
+        X3, Gc, Sh, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -80,6 +84,8 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.rexp = k.take(4 * (int64_t)c->k * (c->m / kPanelRows));
     L.dexp = k.take(4 * (c->w / kPanelRows) * (int64_t)c->k);
     L.X3 = k.take(2 * (int64_t)c->k * c->ldd());   // the third bf16 piece of X (residual refresh)
+    L.Gc = k.take(4 * kw);                           // the carried gradient (fp32)
+    L.Sh = k.take(2 * (int64_t)c->k * c->ldr());     // bf16 image of S
     L.total = k.off;
     return L;
 }
@@ -122,6 +128,20 @@ template <int NT, int ILV, int NS, int WNX>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
         case 0:
+            if constexpr (WNX == 0 && ILV <= 2) {   // carried-gradient forms (one feature block)
+                if (mode && c->gm_cur == 1) {
+                    hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
+                                       dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+                    LAUNCH_CHECK("k_panel_pass1");
+                    break;
+                }
+                if (mode && c->gm_cur == 2) {
+                    hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX, 0, 2>), dim3((unsigned)(c->w / kPanelRows)),
+                                       dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+                    LAUNCH_CHECK("k_panel_pass1");
+                    break;
+                }
+            }
             if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX>), dim3((unsigned)(c->w / kPanelRows)),
                                          dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
             else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX>), dim3((unsigned)(c->w / kPanelRows)),
@@ -167,8 +187,10 @@ int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mod
     return ns == 1 ? panel_launch_ns<1>(c, which, fixed_block, out, mode)
                    : panel_launch_ns<2>(c, which, fixed_block, out, mode);
 }
+bool panel_carry(const bpgl_panel* c) { return c->carry_g && c->nblock == 1 && c->waves[0] == 0; }
 // a solver pass: the lo8 form when the knob selects it for this pass (pass 2 needs the hi + lo direction)
 int panel_pass(bpgl_panel* c, int which) {
+    if (which == 0 && c->gm_cur) return panel_launch(c, 0, -1, nullptr, 1, c->dsplit);   // carried gradient
     const bool l8 = which == 0 ? (c->lo8 & 1) != 0 : ((c->lo8 & 2) != 0 && c->dsplit == 2);
     if (l8) return c->dsplit == 1 ? panel_launch_lo8_ns<1>(c, which) : panel_launch_lo8_ns<2>(c, which);
     return panel_launch(c, which, -1, nullptr, 1, c->dsplit);
@@ -190,10 +212,14 @@ void panel_ev(bpgl_panel* c, int64_t it, int kind, int end) {
     }
     (void)hipEventRecord(c->evs[idx], c->stream);
 }
-int panel_iteration(bpgl_panel* c, int64_t it) {
+// exact: with the carried gradient, this iteration computes G = A^T R exactly (and stores it)
+int panel_iteration(bpgl_panel* c, int64_t it, bool exact = false) {
     int rc;
+    c->gm_cur = panel_carry(c) ? (exact ? 1 : 2) : 0;
     panel_ev(c, it, 0, 0);
-    if ((rc = panel_pass(c, 0))) return rc;
+    rc = panel_pass(c, 0);
+    c->gm_cur = 0;
+    if (rc) return rc;
     panel_ev(c, it, 0, 1);
     panel_ev(c, it, 1, 0);
     if ((rc = panel_pass(c, 1))) return rc;
@@ -275,6 +301,11 @@ int panel_rexp(bpgl_panel* c) {
     return 0;
 }
 
+void drop_graphs(bpgl_panel* c) {
+    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    if (c->gexec_ref) { (void)hipGraphExecDestroy(c->gexec_ref); c->gexec_ref = nullptr; }
+}
+
 int panel_ready(const bpgl_panel* c) {
     if (!c) return fail(BPGL_E_ARG, "null panel context");
     if (!c->bound) return fail(BPGL_E_STATE, "bpgl_panel_bind has not been called");
@@ -328,7 +359,7 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
 void bpgl_panel_destroy(bpgl_panel* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);   // destroy path: nothing to report to
-    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    drop_graphs(c);
     for (auto e : c->evs) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -377,6 +408,7 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.err_rhs = (double*)(s + L.err_rhs);
     p.cnt = (unsigned long long*)(s + L.cnt);
     p.amax = (unsigned*)(s + L.amax);
+    p.Gc = (float*)(s + L.Gc);
     p.rexp = (int*)(s + L.rexp);
     p.dexp = (int*)(s + L.dexp);
     p.wt = c->wt;
@@ -385,7 +417,7 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     c->bound = true;
     c->have_diag = false;
     c->solver = false;
-    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    drop_graphs(c);
     return 0;
 }
 
@@ -449,24 +481,30 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     HIP_TRY(hipMemsetAsync(p.cnt, 0, 8 * (int64_t)c->k, c->stream));   // arrival counters start at 0
     hipLaunchKernelGGL(k_panel_reset_state, dim3(1), dim3(64), 0, c->stream, c->p);
     LAUNCH_CHECK("k_panel_reset_state");
-    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    p.Sh = panel_carry(c) ? (__bf16*)((char*)p.st + (panel_layout(c).Sh - panel_layout(c).st)) : nullptr;
+    drop_graphs(c);
     if (use_graph) {
-        hipGraph_t graph = nullptr;
-        const bool was = c->timing;
-        c->timing = false;
-        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        rc = 0;
-        for (int k = 0; k < kGraphIters && !rc; ++k) rc = panel_iteration(c, 0);
-        hipError_t ec = hipStreamEndCapture(c->stream, &graph);
-        c->timing = was;
-        if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
-        if (ec != hipSuccess) return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
-        hipError_t ei = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (ei != hipSuccess) return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
-        // uploaded here, so the first replay in a caller's timed region pays no upload
-        if ((ei = hipGraphUpload(c->gexec, c->stream)) != hipSuccess)
-            return fail(BPGL_E_HIP, "hipGraphUpload: %s", hipGetErrorString(ei));
+        // kGraphIters iterations; with the carried gradient a second graph whose first iteration is
+        // the exact one (bpgl_panel_step replays it at every g_period-th iteration)
+        for (int g = 0; g < (panel_carry(c) ? 2 : 1); ++g) {
+            hipGraph_t graph = nullptr;
+            const bool was = c->timing;
+            c->timing = false;
+            HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            rc = 0;
+            for (int k = 0; k < kGraphIters && !rc; ++k) rc = panel_iteration(c, 0, g == 1 && k == 0);
+            hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+            c->timing = was;
+            if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+            if (ec != hipSuccess) return fail(BPGL_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
+            hipGraphExec_t& ge = g ? c->gexec_ref : c->gexec;
+            hipError_t ei = hipGraphInstantiate(&ge, graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            if (ei != hipSuccess) return fail(BPGL_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+            // uploaded here, so the first replay in a caller's timed region pays no upload
+            if ((ei = hipGraphUpload(ge, c->stream)) != hipSuccess)
+                return fail(BPGL_E_HIP, "hipGraphUpload: %s", hipGetErrorString(ei));
+        }
     }
     c->solver = true;
     c->timed_iters = 0;
@@ -485,12 +523,14 @@ int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
     while (i < n_iter) {
         if (refresh && c->t_host > 0 && c->t_host % c->r_period == 0 && c->last_refresh != c->t_host)
             if ((rc = panel_refresh(c))) return rc;
+        // carried gradient: every g_period-th iteration (the first included) computes G exactly
+        const bool exact = panel_carry(c) && c->t_host % c->g_period == 0;
         if (!c->timing && c->gexec && i + kGraphIters <= n_iter && c->t_host % kGraphIters == 0) {
-            HIP_TRY(hipGraphLaunch(c->gexec, c->stream));
+            HIP_TRY(hipGraphLaunch(exact ? c->gexec_ref : c->gexec, c->stream));
             i += kGraphIters;
             c->t_host += kGraphIters;
         } else {
-            if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0))) return rc;
+            if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0, exact))) return rc;
             if (c->timing) c->timed_iters++;
             ++i;
             ++c->t_host;
@@ -571,6 +611,16 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else if (!strcmp(key, "d_split")) {
         if (value != 1 && value != 2) return fail(BPGL_E_ARG, "d_split must be 1 or 2");
         c->dsplit = (int)value;
+    } else if (!strcmp(key, "carry_g")) {
+        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "carry_g must be 0 or 1");
+        if (value && c->nblock != 1) return fail(BPGL_E_ARG, "carry_g needs one feature block");
+        c->carry_g = (int)value;
+        c->solver = false;   // the graphs and the operand image depend on it: a reset must follow
+    } else if (!strcmp(key, "g_refresh")) {
+        if (value < kGraphIters || value % kGraphIters)
+            return fail(BPGL_E_ARG, "g_refresh must be a positive multiple of %d", kGraphIters);
+        c->g_period = value;
+        c->solver = false;
     } else if (!strcmp(key, "lo8")) {
         if (value < 0 || value > 3) return fail(BPGL_E_ARG, "lo8 is a mask: 1 pass 1 (residual), 2 pass 2 (direction)");
         if ((value & 2) && (c->w / c->kchunks) % (2 * kPanelK))
@@ -594,7 +644,7 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     } else {
         return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     }
-    if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+    drop_graphs(c);
     return 0;
 }
 
@@ -609,6 +659,8 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else if (!strcmp(key, "op_pad")) *value = c->op_pad;
     else if (!strcmp(key, "lo8")) *value = c->lo8;
+    else if (!strcmp(key, "carry_g")) *value = c->carry_g;
+    else if (!strcmp(key, "g_refresh")) *value = c->g_period;
     else if (!strcmp(key, "r_refresh")) *value = c->r_period;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;

@@ -335,7 +335,7 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * on the objective (the gradient pass, hi + lo always, sets the fixed point;
  * profiles/r04/accuracy); short runs follow slightly different trajectories.
  * bpgl_panel_mtm / _mm always use hi + lo operands.  bpgl_panel_get_tuning reads
- * "interleave1", "interleave2", "d_split", "lo8", "r_refresh".
+ * "interleave1", "interleave2", "d_split", "lo8", "r_refresh", "carry_g", "g_refresh".
  * "lo8" (mask; a reset must follow): the lo piece of the residual (bit 0, pass 1)
  * and of the direction (bit 1, pass 2) on block-scaled e4m3 MFMA
  * (v_mfma_scale_f32_16x16x128_f8f6f4, twice the bf16 rate) against an e4m3 image of
@@ -345,7 +345,14 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * of the oracle instead of 2e-5).  With bit 1 the product S no longer equals A D'
  * exactly, so the incrementally updated residual is recomputed exactly (R = A X - B
  * from X's three bf16 pieces) every "r_refresh" iterations (default 128; 0 = never;
- * a multiple of 8).  lo8 passes use the interleave 0 / 1 / 2 mainloops with 8 waves. */
+ * a multiple of 8).  lo8 passes use the interleave 0 / 1 / 2 mainloops with 8 waves.
+ * "carry_g" (0 / 1, one feature block, not on a solver-mode context; a reset must
+ * follow): the gradient is carried in fp32, G_t = G_{t-1} + gamma_{t-1} A^T S_{t-1}
+ * with S_{t-1} = A D'_{t-1} the previous iteration's product (its bf16 image, one
+ * MFMA product in pass 1 instead of the residual's two), and recomputed exactly
+ * from R (hi + lo) every "g_refresh" iterations (default 64, a multiple of 8) --
+ * the single-RHS path's carried gradient.  Opt-in; DESIGN.md 3b has its measured
+ * speed and 1000-iteration accuracy. */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_get_tuning(const bpgl_panel* ctx, const char* key, int64_t* value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);

@@ -9,7 +9,7 @@ against the oracle fixture, and over all 128 RHS the x / objective difference ag
 hi + lo run (lo8 = 0), plus the drift |R - (A X - B)| of the incrementally updated residual at the
 end of the run.  One JSON line per setting.
 
-Usage (GPU box, repo root): python3 tools/panel_lo8_accuracy.py [ITERS] [lo8:r_refresh[:d_split] ...]
+Usage (GPU box, repo root): python3 tools/panel_lo8_accuracy.py [ITERS] [lo8:r_refresh[:d_split[:carry_g[:g_refresh]]] ...]
 """
 import json
 import os
@@ -25,7 +25,8 @@ def main():
     args = sys.argv[1:]
     it = int(args.pop(0)) if args and ":" not in args[0] else 1000
     settings = [tuple(int(v) for v in a.split(":")) for a in args] or [(0, 0), (1, 0), (2, 128), (3, 128)]
-    settings = [t if len(t) == 3 else t + (2,) for t in settings]   # lo8:r_refresh[:d_split]
+    # lo8:r_refresh[:d_split[:carry_g[:g_refresh]]]
+    settings = [tuple(t) + (2, 0, 64)[len(t) - 2:] if len(t) < 5 else t for t in settings]
     import numpy as np
     import torch
     import hash_instance as H
@@ -46,10 +47,12 @@ def main():
         R = A64 @ Xd - B
         return (0.5 * (R * R).sum(dim=0) + muv * Xd.abs().sum(dim=0)).cpu().numpy(), R
     base = None
-    for lo8, rr, ds in settings:
+    for lo8, rr, ds, cg, gp in settings:
         pl.set_tuning("lo8", lo8)
         pl.set_tuning("r_refresh", rr)
         pl.set_tuning("d_split", ds)
+        pl.set_tuning("carry_g", cg)
+        pl.set_tuning("g_refresh", gp)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         res = pl.run(B, mu, it)
@@ -59,13 +62,13 @@ def main():
         torch.cuda.synchronize()
         Rdev = pl.residual_device().t()
         drift = float((Rdev - Rex).abs().max() / Rex.abs().max())
-        row = {"lo8": lo8, "r_refresh": rr, "d_split": ds, "iters": it, "seconds_incl_setup": el,
+        row = {"lo8": lo8, "r_refresh": rr, "d_split": ds, "carry_g": cg, "g_refresh": gp, "iters": it, "seconds_incl_setup": el,
                "refreshes": pl.stat("refreshes"), "residual_drift_rel_max": drift}
         for r in fx["rhs"]:
             r = int(r)
             row[f"x_rel_vs_oracle_{r}"] = float(np.linalg.norm(X[:, r] - fx[f"x_{r}"]) / np.linalg.norm(fx[f"x_{r}"]))
             row[f"objective_rel_vs_oracle_{r}"] = float(abs(f[r] - fx[f"objective_{r}"]) / fx[f"objective_{r}"])
-        if base is None and lo8 == 0 and ds == 2:
+        if base is None and lo8 == 0 and cg == 0:
             base = (X, f)
         elif base is not None:
             dx = np.linalg.norm(X - base[0], axis=0) / np.maximum(np.linalg.norm(base[0], axis=0), 1e-300)
