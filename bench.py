@@ -642,13 +642,14 @@ def panel_bytes_pass(m, w, k):
     return 2 * m * w + 4 * k * (m + w) + 4 * k * (m + w)
 
 
-def panel_fill_bytes(m, w, k, which, d_split=2):
+def panel_fill_bytes(m, w, k, which, d_split=2, r_pieces=2):
     """Bytes through the CUs' LDS-DMA path per launch of panel pass `which` (1 or 2): every block
     streams its A tile and the k-wide operand over its K range -- pass 1: w/256 blocks, each the
-    residual's hi + lo bf16 pieces over all m rows; pass 2: m/256 row blocks x the column chunks,
+    residual's hi + lo bf16 pieces over all m rows (r_pieces 2; with the carried gradient the bf16 S
+    alone, 1 + 2 / g_refresh on average); pass 2: m/256 row blocks x the column chunks,
     together the direction's d_split pieces over all w columns once per row block."""
     if which == 1:
-        return 2 * m * w + (w // 256) * 2 * 2 * k * m
+        return 2 * m * w + int((w // 256) * r_pieces * 2 * k * m)
     return 2 * m * w + (m // 256) * d_split * 2 * k * w
 
 
@@ -716,12 +717,12 @@ def main_panel(args):
     w = pl.MAT_WIDTH
     dom = max(("pass1_mfma", "pass2_mfma"), key=lambda q: kms[q])
     pb = panel_bytes_pass(m, w, k)
-    fill_bytes = panel_fill_bytes(m, w, k, 1 if dom == "pass1_mfma" else 2, d_split)
     achieved = pb / (kms[dom] * 1e-3) / 1e9
     # MFMA work of the dominant pass: the residual always enters as hi + lo, the direction
     # as hi + lo (d_split 2) or hi alone (d_split 1); with carry_g pass 1 runs the bf16 S product and,
     # every g_refresh iterations, the hi + lo residual products
     p1_products = (1 + 2 / g_period) if carry else 2
+    fill_bytes = panel_fill_bytes(m, w, k, 1 if dom == "pass1_mfma" else 2, d_split, p1_products)
     flops = 2 * m * w * k * (p1_products if dom == "pass1_mfma" else d_split)
     tflops = flops / (kms[dom] * 1e-3) / 1e12
     iters_s = args.steps / el_graph

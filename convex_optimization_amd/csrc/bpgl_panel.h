@@ -102,7 +102,8 @@ struct PanelParams {
     int wt;             // write-through store sites: 1 pass-1 epilogue (x, D'), 2 pass-2 slab, 4 S, 8 R
     // carried gradient (the "carry_g" knob, one feature block): G_t = G_{t-1} + gamma_{t-1} A^T S_{t-1}
     float* Gc;          // [k][w]   the carried gradient (fp32)
-    __bf16* Sh;         // [k][ldr] bf16 image of S (k_panel_reduce), pass 1's operand in a carried iteration
+    __bf16* Sh;         // [k][ldr] pass 1's operand in a carried iteration: bf16(V), V = gamma S + E (k_panel_update)
+    float* Ec;          // [k][m]   V - bf16(V): the rounding error fed into the next carried operand
     // e4m3 lo products (the "lo8" knob, section "lo8" below)
     unsigned* amax;     // float bits of max |A| (k_panel_diag)
     int* rexp;          // [k][m / 256]   frexp exponent of max |R| per 256-row group (update, reset, refresh)
@@ -957,7 +958,9 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 // per RHS and block.  The wave owns output rows c0 + 64 wm .. (A columns) x RHS tiles wn * NTW ..;
 // T threads per block; smem holds at least 4 * k * 3 doubles and is free (after a barrier).
 // GM (carried gradient, one feature block): 0 -- g is the product (A^T R); 1 -- the same, also stored as
-// the carried G; 2 -- the product is U = A^T S_{t-1} and g = G + gamma_{t-1} U, stored back
+// the carried G; 2 -- the product is U = A^T bf16(V_{t-1}) and g = G + U, stored back.  V = gamma S + E
+// (k_panel_update) carries the previous roundings forward (error feedback), so the images' sum tracks
+// R_t - R_exact to one bf16 rounding of the last step instead of accumulating one per step
 template <int NTW, int EPI, int DS, int GM = 0>
 __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int mb, long long c0, int wm, int wn,
                                                      int T, f32x4 (&acc)[4][NTW], char* smem,
@@ -988,7 +991,6 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
         const double mu = p.mu[rhs];
         const double gprev = fx ? p.gamma[rhs] : 0.0;
-        const double gcar = GM == 2 ? p.gamma[rhs] : 0.0;   // gamma_{t-1}: G_t = G_{t-1} + gamma_{t-1} U
         double sbx = 0.0, sx = 0.0, err = 0.0, dmax = 0.0;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
@@ -1018,7 +1020,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 double g = (double)acc[mt][nt][r];
-                if constexpr (GM == 2) g = (double)gs[r] + gcar * g;
+                if constexpr (GM == 2) g = (double)gs[r] + g;
                 if constexpr (GM != 0) gs[r] = (float)g;
                 const double x = (double)xs[r];
                 const long long kx = (long long)mb * p.w + j + r;
@@ -1089,7 +1091,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
     f32x4 acc[4][G::NTW];
-    if constexpr (GM == 2) {   // carried iteration: U = A^T S_{t-1} from the bf16 image of S alone
+    if constexpr (GM == 2) {   // carried iteration: U = A^T bf16(V_{t-1}), one bf16 operand
         if constexpr (ILV >= 2)
             panel_mainloop_pipe<NT, 1, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
                                                (int)(p.m / kPanelK), acc);
@@ -1242,11 +1244,6 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
         const long long e = (long long)rhs * p.m + i;
         wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e, make_double2(s[0], s[1]));
         wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e + 2, make_double2(s[2], s[3]));
-        if (mode && p.Sh) {   // the carried gradient's operand for the next pass 1
-            typedef __bf16 bf16x4s __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<bf16x4s*>(p.Sh + (long long)rhs * p.ldr + i) =
-                bf16x4s{to_bf16((float)s[0]), to_bf16((float)s[1]), to_bf16((float)s[2]), to_bf16((float)s[3])};
-        }
         if (mode) {
             rs = fma(r01.x, s[0], rs); rs = fma(r01.y, s[1], rs);
             rs = fma(r23.x, s[2], rs); rs = fma(r23.y, s[3], rs);
@@ -1349,6 +1346,27 @@ __device__ __forceinline__ void panel_put_rexp(const PanelParams& p, unsigned v,
     if ((threadIdx.x & 63) == 0) p.rexp[v / 64] = panel_frexp(mx);
 }
 
+// carried gradient (one feature block): the next pass 1's operand V = gamma S + E (cflag & 3 == 1; 2: the
+// iteration's G was exact, E restarts at 0), its bf16 image to Sh and the rounding error back to E;
+// cflag & 4: R's hi / lo images are not written (no exact pass 1 reads them before the next update)
+__device__ __forceinline__ void panel_put_carry(const PanelParams& p, int cflag, long long e, long long re,
+                                                double g, const double2& s01, const double2& s23) {
+    typedef __bf16 bf16x4c __attribute__((ext_vector_type(4)));
+    float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((cflag & 3) == 1) e4 = *reinterpret_cast<const float4*>(p.Ec + e);
+    const double v[4] = {(double)e4.x + g * s01.x, (double)e4.y + g * s01.y, (double)e4.z + g * s23.x,
+                         (double)e4.w + g * s23.y};
+    __bf16 h[4];
+    float r[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        h[q] = to_bf16((float)v[q]);
+        r[q] = (float)(v[q] - (double)(float)h[q]);
+    }
+    *reinterpret_cast<bf16x4c*>(p.Sh + re) = bf16x4c{h[0], h[1], h[2], h[3]};
+    *reinterpret_cast<float4*>(p.Ec + e) = make_float4(r[0], r[1], r[2], r[3]);
+}
+
 // x_j += gamma_j D'_j ; Ax_j += gamma_j S_j ; R = sum_b Ax_b - B ; split R.
 // Work units: u < ux -> 8 consecutive x elements ([k][w], 16-B Dh (+ Dl when DS = 2) loads);
 // ux <= u < ux + ur -> 4 consecutive residual rows ([k][m]).  Also bumps t.  k*w and k*m <
@@ -1356,8 +1374,9 @@ __device__ __forceinline__ void panel_put_rexp(const PanelParams& p, unsigned v,
 // NB1 (one feature block): R_j += gamma_j S_j directly -- R = Ax - B with a single block, so Ax
 // and B need not be read or written (28 instead of 44 bytes per residual element); Ax is then not
 // maintained (nothing reads it with one block).
+// cflag: the carried gradient's operand and R's images (panel_put_carry; 0 none).
 template <int DS, bool NB1>
-__global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
+__global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p, int cflag) {
     const int mb = (int)p.st->cur_mb;   // p.st->t is advanced by block 0 of this launch
     const long long nx = (long long)p.k * p.w, nr = (long long)p.k * p.m;
     const unsigned ux = (unsigned)(nx / 8), ur = (unsigned)(nr / 4);
@@ -1404,6 +1423,7 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
                 r[2] = r23.x + g * s23.x; r[3] = r23.y + g * s23.y;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) split_bf16(r[q], hi[q], lo[q]);
+                if (cflag) panel_put_carry(p, cflag, e, re, g, s01, s23);
             } else {
                 double* ap = p.Ax + (long long)mb * nr + e;
                 double a[4], acc[4];
@@ -1424,8 +1444,10 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
             }
             wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
             wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
-            wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
-            wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+            if (!(cflag & 4)) {
+                wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+                wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+            }
             panel_put_rexp(p, v, r);
         }
     }
@@ -1435,7 +1457,7 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p) {
 // One feature block: R_j += gamma_j S_j (= Ax_j + gamma_j S_j - B_j; Ax is not kept) and its
 // hi/lo split; x += gamma D' is left pending for the next pass-1 epilogue (or k_panel_flush).
 // A thread owns 4 consecutive residual rows.  Also bumps t.
-__global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p) {
+__global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p, int cflag) {
     const long long nr = (long long)p.k * p.m;
     const unsigned ur = (unsigned)(nr / 4), m4 = (unsigned)(p.m / 4);
     typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
@@ -1449,13 +1471,16 @@ __global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p) {
         const double2 s01 = *reinterpret_cast<const double2*>(p.S + e);
         const double2 s23 = *reinterpret_cast<const double2*>(p.S + e + 2);
         const double r[4] = {r01.x + g * s01.x, r01.y + g * s01.y, r23.x + g * s23.x, r23.y + g * s23.y};
+        if (cflag) panel_put_carry(p, cflag, e, re, g, s01, s23);
         __bf16 hi[4], lo[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) split_bf16(r[q], hi[q], lo[q]);
         wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
         wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
-        wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
-        wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+        if (!(cflag & 4)) {
+            wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+            wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+        }
         panel_put_rexp(p, v, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, true);

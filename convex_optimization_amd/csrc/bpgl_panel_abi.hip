@@ -38,7 +38,7 @@ struct bpgl_panel {
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
-    int carry_g = 0;              // carried gradient, one feature block ("carry_g" knob)
+    int carry_g = 1;              // carried gradient, one feature block ("carry_g" knob; ignored for nblock > 1)
     int64_t g_period = 64;        // exact gradient every g_period iterations ("g_refresh" knob)
     int gm_cur = 0;               // pass-1 form of the launch being enqueued: 0 plain, 1 exact + store G, 2 carried
     hipGraphExec_t gexec_ref = nullptr;   // carry_g: a graph whose first iteration is the exact-gradient one
@@ -55,7 +55,7 @@ namespace {
 
 struct PanelLayout {
     int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, amax, rexp, dexp,
-        X3, Gc, Sh, total;
+        X3, Gc, Sh, Ec, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -85,7 +85,8 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.dexp = k.take(4 * (c->w / kPanelRows) * (int64_t)c->k);
     L.X3 = k.take(2 * (int64_t)c->k * c->ldd());   // the third bf16 piece of X (residual refresh)
     L.Gc = k.take(4 * kw);                           // the carried gradient (fp32)
-    L.Sh = k.take(2 * (int64_t)c->k * c->ldr());     // bf16 image of S
+    L.Sh = k.take(2 * (int64_t)c->k * c->ldr());     // the carried product's bf16 operand
+    L.Ec = k.take(4 * km);                           // its rounding error, fed into the next one (fp32)
     L.total = k.off;
     return L;
 }
@@ -128,7 +129,7 @@ template <int NT, int ILV, int NS, int WNX>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
         case 0:
-            if constexpr (WNX == 0 && ILV <= 2) {   // carried-gradient forms (one feature block)
+            {   // carried-gradient forms (one feature block)
                 if (mode && c->gm_cur == 1) {
                     hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
                                        dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
@@ -187,7 +188,7 @@ int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mod
     return ns == 1 ? panel_launch_ns<1>(c, which, fixed_block, out, mode)
                    : panel_launch_ns<2>(c, which, fixed_block, out, mode);
 }
-bool panel_carry(const bpgl_panel* c) { return c->carry_g && c->nblock == 1 && c->waves[0] == 0; }
+bool panel_carry(const bpgl_panel* c) { return c->carry_g && c->nblock == 1; }
 // a solver pass: the lo8 form when the knob selects it for this pass (pass 2 needs the hi + lo direction)
 int panel_pass(bpgl_panel* c, int which) {
     if (which == 0 && c->gm_cur) return panel_launch(c, 0, -1, nullptr, 1, c->dsplit);   // carried gradient
@@ -212,10 +213,15 @@ void panel_ev(bpgl_panel* c, int64_t it, int kind, int end) {
     }
     (void)hipEventRecord(c->evs[idx], c->stream);
 }
-// exact: with the carried gradient, this iteration computes G = A^T R exactly (and stores it)
-int panel_iteration(bpgl_panel* c, int64_t it, bool exact = false) {
+// exact: with the carried gradient, this iteration computes G = A^T R exactly (and stores it);
+// split_r: the update writes R's hi / lo images (with the carried gradient only the exact pass 1 reads
+// them, so only an iteration followed by an exact one needs to)
+int panel_iteration(bpgl_panel* c, int64_t it, bool exact = false, bool split_r = true) {
     int rc;
     c->gm_cur = panel_carry(c) ? (exact ? 1 : 2) : 0;
+    // the update's carried-gradient operand: 0 none, 1 V = E + gamma S, 2 V = gamma S (G is exact now);
+    // + 4: skip R's hi / lo images
+    const int cflag = (c->gm_cur == 0 ? 0 : c->gm_cur == 1 ? 2 : 1) | (c->gm_cur && !split_r ? 4 : 0);
     panel_ev(c, it, 0, 0);
     rc = panel_pass(c, 0);
     c->gm_cur = 0;
@@ -230,17 +236,17 @@ int panel_iteration(bpgl_panel* c, int64_t it, bool exact = false) {
     panel_ev(c, it, 4, 0);
     if (c->nblock == 1 && c->defer_x) {   // R only; x += gamma D' rides on the next pass-1 epilogue (or the flush)
         const dim3 ug((unsigned)std::min<int64_t>(cdiv((int64_t)c->k * c->m / 4, kThreads), 8192));
-        hipLaunchKernelGGL(k_panel_update1, ug, dim3(kThreads), 0, c->stream, c->p);
+        hipLaunchKernelGGL(k_panel_update1, ug, dim3(kThreads), 0, c->stream, c->p, cflag);
     } else {
         const int64_t n = (int64_t)c->k * c->w / 8 + (int64_t)c->k * c->m / 4;   // work units
         const dim3 ug((unsigned)std::min<int64_t>(cdiv(n, kThreads), 8192));
         const bool nb1 = c->nblock == 1;
         if (c->dsplit == 1) {
-            if (nb1) hipLaunchKernelGGL((k_panel_update<1, true>), ug, dim3(kThreads), 0, c->stream, c->p);
-            else hipLaunchKernelGGL((k_panel_update<1, false>), ug, dim3(kThreads), 0, c->stream, c->p);
+            if (nb1) hipLaunchKernelGGL((k_panel_update<1, true>), ug, dim3(kThreads), 0, c->stream, c->p, cflag);
+            else hipLaunchKernelGGL((k_panel_update<1, false>), ug, dim3(kThreads), 0, c->stream, c->p, cflag);
         } else {
-            if (nb1) hipLaunchKernelGGL((k_panel_update<2, true>), ug, dim3(kThreads), 0, c->stream, c->p);
-            else hipLaunchKernelGGL((k_panel_update<2, false>), ug, dim3(kThreads), 0, c->stream, c->p);
+            if (nb1) hipLaunchKernelGGL((k_panel_update<2, true>), ug, dim3(kThreads), 0, c->stream, c->p, cflag);
+            else hipLaunchKernelGGL((k_panel_update<2, false>), ug, dim3(kThreads), 0, c->stream, c->p, cflag);
         }
     }
     LAUNCH_CHECK("k_panel_update");
@@ -409,6 +415,7 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.cnt = (unsigned long long*)(s + L.cnt);
     p.amax = (unsigned*)(s + L.amax);
     p.Gc = (float*)(s + L.Gc);
+    p.Ec = (float*)(s + L.Ec);
     p.rexp = (int*)(s + L.rexp);
     p.dexp = (int*)(s + L.dexp);
     p.wt = c->wt;
@@ -492,7 +499,9 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
             c->timing = false;
             HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
             rc = 0;
-            for (int k = 0; k < kGraphIters && !rc; ++k) rc = panel_iteration(c, 0, g == 1 && k == 0);
+            // R's images from the graph's last iteration: the next replay may start with the exact one
+            for (int k = 0; k < kGraphIters && !rc; ++k)
+                rc = panel_iteration(c, 0, g == 1 && k == 0, k == kGraphIters - 1);
             hipError_t ec = hipStreamEndCapture(c->stream, &graph);
             c->timing = was;
             if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
@@ -523,14 +532,18 @@ int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
     while (i < n_iter) {
         if (refresh && c->t_host > 0 && c->t_host % c->r_period == 0 && c->last_refresh != c->t_host)
             if ((rc = panel_refresh(c))) return rc;
-        // carried gradient: every g_period-th iteration (the first included) computes G exactly
-        const bool exact = panel_carry(c) && c->t_host % c->g_period == 0;
+        // carried gradient: every g_period-th iteration (the first included) computes G exactly, and so
+        // does the first one after a residual refresh (R jumped to A X - B; G follows it)
+        const bool exact = panel_carry(c) && (c->t_host % c->g_period == 0 || c->last_refresh == c->t_host);
         if (!c->timing && c->gexec && i + kGraphIters <= n_iter && c->t_host % kGraphIters == 0) {
             HIP_TRY(hipGraphLaunch(exact ? c->gexec_ref : c->gexec, c->stream));
             i += kGraphIters;
             c->t_host += kGraphIters;
         } else {
-            if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0, exact))) return rc;
+            const bool next_exact = (c->t_host + 1) % c->g_period == 0 ||
+                                    (refresh && (c->t_host + 1) % c->r_period == 0);
+            if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0, exact, next_exact || i + 1 == n_iter)))
+                return rc;
             if (c->timing) c->timed_iters++;
             ++i;
             ++c->t_host;
@@ -659,7 +672,7 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
     else if (!strcmp(key, "op_pad")) *value = c->op_pad;
     else if (!strcmp(key, "lo8")) *value = c->lo8;
-    else if (!strcmp(key, "carry_g")) *value = c->carry_g;
+    else if (!strcmp(key, "carry_g")) *value = panel_carry(c) ? 1 : 0;   // the form in effect
     else if (!strcmp(key, "g_refresh")) *value = c->g_period;
     else if (!strcmp(key, "r_refresh")) *value = c->r_period;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);

@@ -197,8 +197,8 @@ class PanelLasso:
         """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave' 0-2.
         'd_split' 1 (default) / 2: the solver's direction enters the A D pass as its bf16 rounding (1)
         or as a hi + lo pair (2); both are exact line searches along the direction taken.  'lo8' (mask,
-        opt-in) / 'r_refresh': e4m3 lo products; 'carry_g' (opt-in, one block) / 'g_refresh': the carried
-        fp32 gradient with an exact recompute every g_refresh iterations (include/bpgl.h)."""
+        opt-in) / 'r_refresh': e4m3 lo products; 'carry_g' (default 1, one block) / 'g_refresh': the
+        carried fp32 gradient with an exact recompute every g_refresh iterations (include/bpgl.h)."""
         N.check(_lib().bpgl_panel_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_panel_set_tuning")
 
     def get_tuning(self, key):

@@ -58,7 +58,8 @@ const char* bpgl_last_error(void);
  *   200 (0.2.0): + bpgl_stream_create / bpgl_stream_destroy; bpgl_iterate always synchronises
  *                the solver stream before returning; the "onepass_cache_permille" default moved
  *                from 0 to -1 (automatic: 750 when the rank's A block fits the Infinity Cache);
- *                panel tuning key "lo8" (e4m3 lo products) and "r_refresh". */
+ *                panel tuning keys "lo8" (e4m3 lo products), "r_refresh", "carry_g"
+ *                (default 1: the carried gradient, one feature block) and "g_refresh". */
 int bpgl_version(void);
 
 /*
@@ -346,13 +347,17 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * exactly, so the incrementally updated residual is recomputed exactly (R = A X - B
  * from X's three bf16 pieces) every "r_refresh" iterations (default 128; 0 = never;
  * a multiple of 8).  lo8 passes use the interleave 0 / 1 / 2 mainloops with 8 waves.
- * "carry_g" (0 / 1, one feature block, not on a solver-mode context; a reset must
- * follow): the gradient is carried in fp32, G_t = G_{t-1} + gamma_{t-1} A^T S_{t-1}
- * with S_{t-1} = A D'_{t-1} the previous iteration's product (its bf16 image, one
- * MFMA product in pass 1 instead of the residual's two), and recomputed exactly
- * from R (hi + lo) every "g_refresh" iterations (default 64, a multiple of 8) --
- * the single-RHS path's carried gradient.  Opt-in; DESIGN.md 3b has its measured
- * speed and 1000-iteration accuracy. */
+ * "carry_g" (0 / 1; default 1, in effect with one feature block only -- set to 1
+ * with more blocks is an error; a reset must follow a change): the gradient is
+ * carried in fp32, G_t = G_{t-1} + gamma_{t-1} A^T S_{t-1} with S_{t-1} = A D'_{t-1}
+ * the previous iteration's product (its bf16 image: one MFMA product in pass 1
+ * instead of the residual's two), and recomputed exactly from R (hi + lo) every
+ * "g_refresh" iterations (default 64, a multiple of 8) and after every residual
+ * refresh -- the single-RHS path's carried gradient.  Measured at configs[4]: pass 1
+ * 226 -> 196 us, and after 1000 iterations x within 4e-6 of the oracle instead of
+ * 1.9e-5 (fp32 accumulation of small updates instead of re-reading R through its
+ * 2^-17 pieces).  With it, lo8 bit 0 is not used (pass 1 multiplies S).
+ * get_tuning("carry_g") reports the form in effect. */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_get_tuning(const bpgl_panel* ctx, const char* key, int64_t* value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
