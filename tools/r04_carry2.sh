@@ -13,3 +13,4 @@ rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 240 python bench.py --config 4 > $OUT/bench_default.json 2> $OUT/bench_default.err || exit $?
 timeout -k 10 240 python bench.py --config 4 --carry-g 0 > $OUT/bench_cg0.json 2> $OUT/bench_cg0.err || exit $?
 timeout -k 10 240 python bench.py --config 4 --interleave 3 > $OUT/bench_il3.json 2> $OUT/bench_il3.err || exit $?
+timeout -k 10 240 python bench.py --config 4 --defer-x 1 > $OUT/bench_dx1.json 2> $OUT/bench_dx1.err || exit $?
