@@ -29,19 +29,22 @@ def counters(d):
 
 
 def durations(d):
-    out = {}
+    """average launch duration per pass over all of its instantiations (the carried-gradient pass 1
+    runs two: the carried form and, every g_refresh iterations, the exact one), weighted by calls"""
+    tot, calls = defaultdict(float), defaultdict(int)
     for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             for k in ("k_panel_pass1", "k_panel_pass2"):
                 if k in r["Name"]:
-                    out[k] = float(r["AverageNs"]) * 1e-9
-    return out
+                    tot[k] += float(r["TotalDurationNs"]) * 1e-9
+                    calls[k] += int(r["Calls"])
+    return {k: tot[k] / calls[k] for k in tot if calls[k]}
 
 
 def main():
     root = sys.argv[1]
     dur = durations(os.path.join(root, "trace"))
-    res = {"source": "tools/profile_r04.sh (rocprofv3 --pmc, one pass per k; round 4, d_split 1) + kernel trace of bench.py --config 4",
+    res = {"source": os.environ.get("MFMA_SOURCE", "tools/profile_r04b.sh (rocprofv3 --pmc, one pass per k; round 4 defaults: d_split 1, carried gradient) + kernel trace of bench.py --config 4"),
            "simds": SIMDS, "peak_clock_hz": PEAK_HZ}
     for kdir in sorted(glob.glob(os.path.join(root, "k*"))):
         k = os.path.basename(kdir)
