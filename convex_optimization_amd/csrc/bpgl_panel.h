@@ -986,45 +986,92 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
     // arithmetic as k_panel_update's x part, so x is bitwise unchanged by the deferral
     const bool fx = p.st->pending != 0;
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    // every load is issued ahead of the stores it would otherwise wait behind (the compiler cannot
+    // reorder loads past stores through possibly aliasing pointers, and one dependent round trip per
+    // (RHS tile, column group) serialised the epilogue): mu / gamma per RHS tile up front, and X, diag,
+    // rec (and the carried G) one (RHS tile, column group) step ahead of
+    // their use (D' of a pending x update is read at the step itself: defer_x is not the default).
+    // Same arithmetic, same order.
+    const long long jl = c0 + wm * 64 + (lane >> 4) * 4;   // the lane's first column; + 16 mt + r
+    double muv[NTW], gpv[NTW];
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
         const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
-        const double mu = p.mu[rhs];
-        const double gprev = fx ? p.gamma[rhs] : 0.0;
+        muv[nt] = p.mu[rhs];
+        gpv[nt] = fx ? p.gamma[rhs] : 0.0;
+    }
+    auto xptr = [&](int nt, int mt) {
+        return p.X + ((long long)mb * p.k + (wn * NTW + nt) * 16 + (lane & 15)) * p.w + jl + mt * 16;
+    };
+    auto gptr = [&](int nt, int mt) {
+        return p.Gc + (long long)((wn * NTW + nt) * 16 + (lane & 15)) * p.w + jl + mt * 16;
+    };
+    auto dptr = [&](const __bf16* base, int nt, int mt) {
+        return base + (long long)((wn * NTW + nt) * 16 + (lane & 15)) * p.ldd + jl + mt * 16;
+    };
+    auto lddr = [&](const double* base, int mt, double2& a, double2& b) {
+        const long long kx = (long long)mb * p.w + jl + mt * 16;
+        a = *reinterpret_cast<const double2*>(base + kx);
+        b = *reinterpret_cast<const double2*>(base + kx + 2);
+    };
+    double2 dq01, dq23, rq01, rq23;
+    lddr(p.diag, 0, dq01, dq23);
+    lddr(p.rec, 0, rq01, rq23);
+    float4 xq = *reinterpret_cast<const float4*>(xptr(0, 0));
+    float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (GM == 2) gq = *reinterpret_cast<const float4*>(gptr(0, 0));
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+        const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
+        const double mu = muv[nt];
+        const double gprev = gpv[nt];
         double sbx = 0.0, sx = 0.0, err = 0.0, dmax = 0.0;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-            const long long j = c0 + wm * 64 + mt * 16 + (lane >> 4) * 4;   // 4 consecutive columns
-            float* xp = p.X + ((long long)mb * p.k + rhs) * p.w + j;
-            const float4 x4 = *reinterpret_cast<const float4*>(xp);
-            float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+            const long long j = jl + mt * 16;   // 4 consecutive columns
+            // the next step's operands first
+            const int q1 = nt * 4 + mt + 1, nt1 = q1 / 4, mt1 = q1 % 4;
+            float4 xn = xq, gn = gq;
+            double2 dn01 = dq01, dn23 = dq23, rn01 = rq01, rn23 = rq23;
+            if (q1 < NTW * 4) {
+                if constexpr (DS == 1) {   // (with the hi + lo direction the registers are not there: no spills)
+                    lddr(p.diag, mt1, dn01, dn23);
+                    lddr(p.rec, mt1, rn01, rn23);
+                }
+                xn = *reinterpret_cast<const float4*>(xptr(nt1, mt1));
+                if constexpr (GM == 2) gn = *reinterpret_cast<const float4*>(gptr(nt1, mt1));
+            }
+            float xs[4] = {xq.x, xq.y, xq.z, xq.w};
             if (fx) {
-                const bf16x4 ph = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.ldd + j);
-                bf16x4 pl;
-                if constexpr (DS == 2) pl = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.ldd + j);
+                const bf16x4 hq = *reinterpret_cast<const bf16x4*>(dptr(p.Dh, nt, mt));
+                bf16x4 lq;
+                if constexpr (DS == 2) lq = *reinterpret_cast<const bf16x4*>(dptr(p.Dl, nt, mt));
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    double dq = (double)(float)ph[r];
-                    if constexpr (DS == 2) dq += (double)(float)pl[r];
+                    double dq = (double)(float)hq[r];
+                    if constexpr (DS == 2) dq += (double)(float)lq[r];
                     xs[r] = (float)((double)xs[r] + gprev * dq);
                 }
                 wt_put(p.wt & 1, p.X, (long long)p.nblock * p.k * p.w, ((long long)mb * p.k + rhs) * p.w + j,
                        make_float4(xs[0], xs[1], xs[2], xs[3]));
             }
             __bf16 dh[4], dl[4];
-            float gs[4];
-            if constexpr (GM == 2) {
-                const float4 g4 = *reinterpret_cast<const float4*>(p.Gc + (long long)rhs * p.w + j);
-                gs[0] = g4.x; gs[1] = g4.y; gs[2] = g4.z; gs[3] = g4.w;
+            if constexpr (DS == 2) {
+                if (q1 > 1) {   // step 0's came with the prologue
+                    lddr(p.diag, mt, dq01, dq23);
+                    lddr(p.rec, mt, rq01, rq23);
+                }
             }
+            float gs[4] = {gq.x, gq.y, gq.z, gq.w};
+            const double dgv[4] = {dq01.x, dq01.y, dq23.x, dq23.y};
+            const double rcv[4] = {rq01.x, rq01.y, rq23.x, rq23.y};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 double g = (double)acc[mt][nt][r];
                 if constexpr (GM == 2) g = (double)gs[r] + g;
                 if constexpr (GM != 0) gs[r] = (float)g;
                 const double x = (double)xs[r];
-                const long long kx = (long long)mb * p.w + j + r;
-                const double bx = p.rec[kx] * soft_thr(p.diag[kx] * x - g, mu);
+                const double bx = rcv[r] * soft_thr(dgv[r] * x - g, mu);
                 double dprime;
                 dmax = fmax(dmax, fabs(bx - x));
                 if constexpr (DS == 2) {
@@ -1044,6 +1091,8 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
             if constexpr (DS == 2)
                 wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
+            xq = xn; gq = gn;
+            dq01 = dn01; dq23 = dn23; rq01 = rn01; rq23 = rn23;
         }
         // lanes l, l^16, l^32, l^48 share the RHS
         sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
