@@ -961,6 +961,11 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 // the carried G; 2 -- the product is U = A^T bf16(V_{t-1}) and g = G + U, stored back.  V = gamma S + E
 // (k_panel_update) carries the previous roundings forward (error feedback), so the images' sum tracks
 // R_t - R_exact to one bf16 rounding of the last step instead of accumulating one per step
+// BPGL_PANEL_DIAG (timing-only builds, tools/panel_epi_diag.sh; results wrong): bit 0 -- no carried-G
+// store, bit 1 -- no D' store, bit 3 -- no epilogue loop at all (the products are only kept alive)
+#ifndef BPGL_PANEL_DIAG
+#define BPGL_PANEL_DIAG 0
+#endif
 template <int NTW, int EPI, int DS, int GM = 0>
 __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int mb, long long c0, int wm, int wn,
                                                      int T, f32x4 (&acc)[4][NTW], char* smem,
@@ -981,6 +986,15 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         return;
     }
     double* nred = reinterpret_cast<double*>(smem);   // [4 wm][k][4]
+    if constexpr ((BPGL_PANEL_DIAG & 8) != 0) {
+        float sink = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt) sink += acc[mt][nt][0] + acc[mt][nt][1] + acc[mt][nt][2] + acc[mt][nt][3];
+        if (p.k < 0) p.Gc[lane] = sink;
+        return;
+    }
     // one feature block: the previous iteration's x += gamma D' (k_panel_update leaves it
     // pending) is applied here, from the D' this thread is about to overwrite -- the same
     // arithmetic as k_panel_update's x part, so x is bitwise unchanged by the deferral
@@ -990,8 +1004,8 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
     // reorder loads past stores through possibly aliasing pointers, and one dependent round trip per
     // (RHS tile, column group) serialised the epilogue): mu / gamma per RHS tile up front, and X, diag,
     // rec (and the carried G) one (RHS tile, column group) step ahead of
-    // their use (D' of a pending x update is read at the step itself: defer_x is not the default).
-    // Same arithmetic, same order.
+    // their use (D' of a pending x update too with the bf16 direction; with hi + lo at the step
+    // itself, for registers).  Same arithmetic, same order.
     const long long jl = c0 + wm * 64 + (lane >> 4) * 4;   // the lane's first column; + 16 mt + r
     double muv[NTW], gpv[NTW];
 #pragma unroll
@@ -1020,6 +1034,9 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
     float4 xq = *reinterpret_cast<const float4*>(xptr(0, 0));
     float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (GM == 2) gq = *reinterpret_cast<const float4*>(gptr(0, 0));
+    bf16x4 hq1 = {};
+    if constexpr (DS == 1)
+        if (fx) hq1 = *reinterpret_cast<const bf16x4*>(dptr(p.Dh, 0, 0));
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
         const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
@@ -1032,6 +1049,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             // the next step's operands first
             const int q1 = nt * 4 + mt + 1, nt1 = q1 / 4, mt1 = q1 % 4;
             float4 xn = xq, gn = gq;
+            bf16x4 hn1 = hq1;
             double2 dn01 = dq01, dn23 = dq23, rn01 = rq01, rn23 = rq23;
             if (q1 < NTW * 4) {
                 if constexpr (DS == 1) {   // (with the hi + lo direction the registers are not there: no spills)
@@ -1040,11 +1058,13 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 }
                 xn = *reinterpret_cast<const float4*>(xptr(nt1, mt1));
                 if constexpr (GM == 2) gn = *reinterpret_cast<const float4*>(gptr(nt1, mt1));
+                if constexpr (DS == 1)
+                    if (fx) hn1 = *reinterpret_cast<const bf16x4*>(dptr(p.Dh, nt1, mt1));
             }
             float xs[4] = {xq.x, xq.y, xq.z, xq.w};
             if (fx) {
-                const bf16x4 hq = *reinterpret_cast<const bf16x4*>(dptr(p.Dh, nt, mt));
-                bf16x4 lq;
+                bf16x4 hq = hq1, lq;
+                if constexpr (DS == 2) hq = *reinterpret_cast<const bf16x4*>(dptr(p.Dh, nt, mt));
                 if constexpr (DS == 2) lq = *reinterpret_cast<const bf16x4*>(dptr(p.Dl, nt, mt));
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -1086,12 +1106,13 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 const double e = fabs(g - proj(g - x, -mu, mu));
                 err = (e > err || e != e) ? e : err;
             }
-            if constexpr (GM != 0)
+            if constexpr (GM != 0 && (BPGL_PANEL_DIAG & 1) == 0)
                 *reinterpret_cast<float4*>(p.Gc + (long long)rhs * p.w + j) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+            if constexpr ((BPGL_PANEL_DIAG & 2) == 0)
             wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
             if constexpr (DS == 2)
                 wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
-            xq = xn; gq = gn;
+            xq = xn; gq = gn; hq1 = hn1;
             dq01 = dn01; dq23 = dn23; rq01 = rn01; rq23 = rn23;
         }
         // lanes l, l^16, l^32, l^48 share the RHS
