@@ -961,12 +961,90 @@ __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
 // the carried G; 2 -- the product is U = A^T bf16(V_{t-1}) and g = G + U, stored back.  V = gamma S + E
 // (k_panel_update) carries the previous roundings forward (error feedback), so the images' sum tracks
 // R_t - R_exact to one bf16 rounding of the last step instead of accumulating one per step
+// 16-B LDS read by inline asm: the compiler does not tie it to outstanding LDS-DMA (it cannot tell one
+// buffer of the shared array from another and would wait for every DMA in flight); the caller orders
+// it after the DMA it reads (s_waitcnt vmcnt + barrier) and retires it with lds_wait
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned lds_off(const void* ptr) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)ptr;
+}
+__device__ __forceinline__ u32x4 lds_rd128(unsigned addr) {
+    u32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+
+// one (RHS tile, column group) step of the shrink epilogue: the lane's 4 columns of one RHS -- g from
+// the product (+ the carried G), the prox step, D' in DS bf16 pieces, the norm / error partials
+template <int DS, int GM>
+__device__ __forceinline__ void panel_shrink4(const f32x4& acc, const float (&xs)[4], float (&gs)[4],
+                                              const double (&dgv)[4], const double (&rcv)[4], double mu,
+                                              __bf16 (&dh)[4], __bf16 (&dl)[4], double& sbx, double& sx,
+                                              double& err, double& dmax) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double g = (double)acc[r];
+        if constexpr (GM == 2) g = (double)gs[r] + g;
+        if constexpr (GM != 0) gs[r] = (float)g;
+        const double x = (double)xs[r];
+        const double bx = rcv[r] * soft_thr(dgv[r] * x - g, mu);
+        double dprime;
+        dmax = fmax(dmax, fabs(bx - x));
+        if constexpr (DS == 2) {
+            split_bf16(bx - x, dh[r], dl[r]);
+            dprime = (double)(float)dh[r] + (double)(float)dl[r];
+        } else {
+            dh[r] = to_bf16((float)(bx - x));
+            dprime = (double)(float)dh[r];
+        }
+        sbx += fabs(x + dprime);
+        sx += fabs(x);
+        const double e = fabs(g - proj(g - x, -mu, mu));
+        err = (e > err || e != e) ? e : err;
+    }
+}
+// the per-RHS partials of one wave's RHS tile (lanes l, l^16, l^32, l^48 share the RHS) -> nred
+__device__ __forceinline__ void panel_norms_wave(double* nred, int wm, int K, int rhs, double sbx, double sx,
+                                                 double err, double dmax) {
+    const int lane = threadIdx.x & 63;
+    sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
+    sx += __shfl_xor(sx, 16);   sx += __shfl_xor(sx, 32);
+    { double o = __shfl_xor(err, 16); err = (o > err || o != o) ? o : err;
+      o = __shfl_xor(err, 32); err = (o > err || o != o) ? o : err; }
+    dmax = fmax(dmax, __shfl_xor(dmax, 16)); dmax = fmax(dmax, __shfl_xor(dmax, 32));
+    if (lane < 16) {
+        double* d = nred + ((long long)wm * K + rhs) * 4;
+        d[0] = sbx;
+        d[1] = sx;
+        d[2] = err;
+        d[3] = dmax;
+    }
+}
+// the block's norms per RHS from the four column groups' partials (after a barrier)
+__device__ __forceinline__ void panel_norms_out(const PanelParams& p, const double* nred, int T) {
+    const int K = p.k;
+    for (int rhs = threadIdx.x; rhs < K; rhs += T) {
+        double a = 0.0, b = 0.0, e = 0.0, dm = 0.0;
+        for (int q = 0; q < 4; ++q) {
+            const double* d = nred + ((long long)q * K + rhs) * 4;
+            a += d[0];
+            b += d[1];
+            e = (d[2] > e || d[2] != d[2]) ? d[2] : e;
+            dm = fmax(dm, d[3]);
+        }
+        double* dst = p.norms + ((long long)blockIdx.x * p.k + rhs) * 4;
+        dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
+        // the tile's max |D| for the e4m3 scale of the direction's lo piece in pass 2 (lo8)
+        if (p.dexp) p.dexp[(long long)blockIdx.x * p.k + rhs] = panel_frexp(dm);
+    }
+}
+
 // BPGL_PANEL_DIAG (timing-only builds, tools/panel_epi_diag.sh; results wrong): bit 0 -- no carried-G
 // store, bit 1 -- no D' store, bit 3 -- no epilogue loop at all (the products are only kept alive)
 #ifndef BPGL_PANEL_DIAG
 #define BPGL_PANEL_DIAG 0
 #endif
-template <int NTW, int EPI, int DS, int GM = 0>
+template <int NTW, int EPI, int DS, int GM = 0, int NW = 0>
 __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int mb, long long c0, int wm, int wn,
                                                      int T, f32x4 (&acc)[4][NTW], char* smem,
                                                      double* __restrict__ Gout) {
@@ -1000,6 +1078,100 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
     // arithmetic as k_panel_update's x part, so x is bitwise unchanged by the deferral
     const bool fx = p.st->pending != 0;
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    if constexpr (NTW == 4 && NW == 8) {
+        // k = 128, 8 waves: the block's X (and carried G) rows travel HBM -> LDS by LDS-DMA, 1 KiB
+        // per instruction (256 columns x fp32 of one RHS), one RHS tile per phase for both wave
+        // columns (32 rows), two phases in flight -- instead of per-lane 16-B loads whose round trips
+        // left the epilogue latency-bound (≈31 µs of the carried pass 1, BPGL_PANEL_DIAG 8).
+        // diag / rec of the block's 256 columns are staged once.  Same arithmetic, same order.
+        constexpr int RS = 1024 + 16;                 // LDS row stride (+16 B: conflict-free 16-B reads)
+        constexpr int NR = 32;                        // RHS rows per phase
+        constexpr int BUF = (GM == 2 ? 2 : 1) * NR * RS;
+        static_assert(2 * 2 * NR * RS + 6144 + 4 * 128 * 4 * 8 <= 160 * 1024, "LDS budget");
+        char* dgl = smem + 2 * BUF;                   // diag [256], rec [256], mu [128], gamma [128] (fp64)
+        double* nrd = reinterpret_cast<double*>(dgl + 6144);
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        __syncthreads();                              // the mainloop's last LDS reads are done
+        // every operand by LDS-DMA (vmcnt retires in order: a plain load issued after the next
+        // phase's DMA would make its first use wait for that phase too)
+        if (wave < 4)
+            glds16((wave < 2 ? p.diag : p.rec) + (long long)mb * p.w + c0 + (wave & 1) * 128 + lane * 2,
+                   dgl + wave * 1024);
+        else if (wave < 6)
+            glds16((wave == 4 ? p.mu : p.gamma) + lane * 2, dgl + 4096 + (wave - 4) * 1024);
+        auto issue = [&](int nt, char* buf) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = wave * 4 + i;
+                const int rhs = ((r >> 4) * 4 + nt) * 16 + (r & 15);
+                glds16a(p.X + ((long long)mb * p.k + rhs) * p.w + c0 + lane * 4, buf + r * RS);
+                if constexpr (GM == 2) glds16a(p.Gc + (long long)rhs * p.w + c0 + lane * 4, buf + (NR + r) * RS);
+            }
+        };
+        issue(0, smem);
+        issue(1, smem + BUF);
+        constexpr int OPS = GM == 2 ? 8 : 4;          // LDS-DMA instructions of one phase per wave
+        const int rl = wn * 16 + (lane & 15);         // this lane's RHS row within a phase
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            if (nt < 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(OPS) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            const char* buf = smem + (nt & 1) * BUF;
+            const int rhs = (wn * 4 + nt) * 16 + (lane & 15);
+            const double mu = reinterpret_cast<const double*>(dgl + 4096)[rhs];
+            const double gprev = fx ? reinterpret_cast<const double*>(dgl + 5120)[rhs] : 0.0;
+            double sbx = 0.0, sx = 0.0, err = 0.0, dmax = 0.0;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int cc = wm * 64 + mt * 16 + (lane >> 4) * 4;   // column within the block
+                const long long j = c0 + cc;
+                u32x4 vx = lds_rd128(lds_off(buf + rl * RS + cc * 4)), vg = {0u, 0u, 0u, 0u};
+                if constexpr (GM == 2) vg = lds_rd128(lds_off(buf + (NR + rl) * RS + cc * 4));
+                u32x4 vd0 = lds_rd128(lds_off(dgl + cc * 8)), vd1 = lds_rd128(lds_off(dgl + cc * 8 + 16));
+                u32x4 vr0 = lds_rd128(lds_off(dgl + 2048 + cc * 8)), vr1 = lds_rd128(lds_off(dgl + 2048 + cc * 8 + 16));
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vx), "+v"(vg), "+v"(vd0), "+v"(vd1), "+v"(vr0), "+v"(vr1));
+                const float4 x4 = __builtin_bit_cast(float4, vx);
+                float gs[4] = {0.f, 0.f, 0.f, 0.f};
+                if constexpr (GM == 2) {
+                    const float4 g4 = __builtin_bit_cast(float4, vg);
+                    gs[0] = g4.x; gs[1] = g4.y; gs[2] = g4.z; gs[3] = g4.w;
+                }
+                const double2 d01 = __builtin_bit_cast(double2, vd0), d23 = __builtin_bit_cast(double2, vd1);
+                const double2 r01 = __builtin_bit_cast(double2, vr0), r23 = __builtin_bit_cast(double2, vr1);
+                const double dgv[4] = {d01.x, d01.y, d23.x, d23.y};
+                const double rcv[4] = {r01.x, r01.y, r23.x, r23.y};
+                float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+                if (fx) {
+                    const bf16x4 hq = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.ldd + j);
+                    bf16x4 lq;
+                    if constexpr (DS == 2) lq = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.ldd + j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        double dq = (double)(float)hq[r];
+                        if constexpr (DS == 2) dq += (double)(float)lq[r];
+                        xs[r] = (float)((double)xs[r] + gprev * dq);
+                    }
+                    wt_put(p.wt & 1, p.X, (long long)p.nblock * p.k * p.w, ((long long)mb * p.k + rhs) * p.w + j,
+                           make_float4(xs[0], xs[1], xs[2], xs[3]));
+                }
+                __bf16 dh[4], dl[4];
+                panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err, dmax);
+                if constexpr (GM != 0)
+                    *reinterpret_cast<float4*>(p.Gc + (long long)rhs * p.w + j) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+                wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
+                if constexpr (DS == 2)
+                    wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
+            }
+            panel_norms_wave(nrd, wm, K, rhs, sbx, sx, err, dmax);
+            if (nt + 2 < 4) {
+                __syncthreads();                      // every wave is done with this phase's buffer
+                issue(nt + 2, smem + (nt & 1) * BUF);
+            }
+        }
+        __syncthreads();
+        panel_norms_out(p, nrd, T);
+        return;
+    }
     // every load is issued ahead of the stores it would otherwise wait behind (the compiler cannot
     // reorder loads past stores through possibly aliasing pointers, and one dependent round trip per
     // (RHS tile, column group) serialised the epilogue): mu / gamma per RHS tile up front, and X, diag,
@@ -1085,27 +1257,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             float gs[4] = {gq.x, gq.y, gq.z, gq.w};
             const double dgv[4] = {dq01.x, dq01.y, dq23.x, dq23.y};
             const double rcv[4] = {rq01.x, rq01.y, rq23.x, rq23.y};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                double g = (double)acc[mt][nt][r];
-                if constexpr (GM == 2) g = (double)gs[r] + g;
-                if constexpr (GM != 0) gs[r] = (float)g;
-                const double x = (double)xs[r];
-                const double bx = rcv[r] * soft_thr(dgv[r] * x - g, mu);
-                double dprime;
-                dmax = fmax(dmax, fabs(bx - x));
-                if constexpr (DS == 2) {
-                    split_bf16(bx - x, dh[r], dl[r]);
-                    dprime = (double)(float)dh[r] + (double)(float)dl[r];
-                } else {
-                    dh[r] = to_bf16((float)(bx - x));
-                    dprime = (double)(float)dh[r];
-                }
-                sbx += fabs(x + dprime);
-                sx += fabs(x);
-                const double e = fabs(g - proj(g - x, -mu, mu));
-                err = (e > err || e != e) ? e : err;
-            }
+            panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err, dmax);
             if constexpr (GM != 0 && (BPGL_PANEL_DIAG & 1) == 0)
                 *reinterpret_cast<float4*>(p.Gc + (long long)rhs * p.w + j) = make_float4(gs[0], gs[1], gs[2], gs[3]);
             if constexpr ((BPGL_PANEL_DIAG & 2) == 0)
@@ -1115,35 +1267,10 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             xq = xn; gq = gn; hq1 = hn1;
             dq01 = dn01; dq23 = dn23; rq01 = rn01; rq23 = rn23;
         }
-        // lanes l, l^16, l^32, l^48 share the RHS
-        sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
-        sx += __shfl_xor(sx, 16);   sx += __shfl_xor(sx, 32);
-        { double o = __shfl_xor(err, 16); err = (o > err || o != o) ? o : err;
-          o = __shfl_xor(err, 32); err = (o > err || o != o) ? o : err; }
-        dmax = fmax(dmax, __shfl_xor(dmax, 16)); dmax = fmax(dmax, __shfl_xor(dmax, 32));
-        if (lane < 16) {
-            double* d = nred + ((long long)wm * K + rhs) * 4;
-            d[0] = sbx;
-            d[1] = sx;
-            d[2] = err;
-            d[3] = dmax;
-        }
+        panel_norms_wave(nred, wm, K, rhs, sbx, sx, err, dmax);
     }
     __syncthreads();
-    for (int rhs = threadIdx.x; rhs < K; rhs += T) {
-        double a = 0.0, b = 0.0, e = 0.0, dm = 0.0;
-        for (int q = 0; q < 4; ++q) {
-            const double* d = nred + ((long long)q * K + rhs) * 4;
-            a += d[0];
-            b += d[1];
-            e = (d[2] > e || d[2] != d[2]) ? d[2] : e;
-            dm = fmax(dm, d[3]);
-        }
-        double* dst = p.norms + ((long long)blockIdx.x * p.k + rhs) * 4;
-        dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
-        // the tile's max |D| for the e4m3 scale of the direction's lo piece in pass 2 (lo8)
-        if (p.dexp) p.dexp[(long long)blockIdx.x * p.k + rhs] = panel_frexp(dm);
-    }
+    panel_norms_out(p, nred, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -1168,7 +1295,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
         else
             panel_mainloop<NT, 1, ILV, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
                                                (int)(p.m / kPanelK), acc);
-        panel_pass1_epilogue<G::NTW, EPI, DS, 2>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
+        panel_pass1_epilogue<G::NTW, EPI, DS, 2, G::NW>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
         return;
     } else if constexpr (L8 && ILV >= 2)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
         panel_mainloop_pipe_lo8<NT, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
@@ -1188,7 +1315,7 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
         panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                            (int)(p.m / kPanelK), acc);
 
-    panel_pass1_epilogue<G::NTW, EPI, DS, GM>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
+    panel_pass1_epilogue<G::NTW, EPI, DS, GM, G::NW>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
 }
 
 // ---------------------------------------------------------------------------
