@@ -1156,8 +1156,9 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 }
                 __bf16 dh[4], dl[4];
                 panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err, dmax);
-                if constexpr (GM != 0)
-                    *reinterpret_cast<float4*>(p.Gc + (long long)rhs * p.w + j) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+                if constexpr (GM != 0)   // read again only next iteration, after all of A: non-temporal
+                    __builtin_nontemporal_store(f32x4{gs[0], gs[1], gs[2], gs[3]},
+                                                reinterpret_cast<f32x4*>(p.Gc + (long long)rhs * p.w + j));
                 wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
                 if constexpr (DS == 2)
                     wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
