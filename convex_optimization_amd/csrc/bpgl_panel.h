@@ -1108,7 +1108,23 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 if constexpr (GM == 2) glds16a(p.Gc + (long long)rhs * p.w + c0 + lane * 4, buf + (NR + r) * RS);
             }
         };
+        // a pending x update (defer_x) with the bf16 direction: each phase's D' goes to registers just
+        // before the phase's DMA, so the phase wait covers it (vmcnt retires in order)
+        bf16x4 dpre[2][4] = {};
+        auto lddp = [&](int nt) {
+            if constexpr (DS == 1) {
+                if (fx) {
+                    const int rq = (wn * 4 + nt) * 16 + (lane & 15);
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt)
+                        dpre[nt & 1][mt] = *reinterpret_cast<const bf16x4*>(
+                            p.Dh + (long long)rq * p.ldd + c0 + wm * 64 + mt * 16 + (lane >> 4) * 4);
+                }
+            }
+        };
+        lddp(0);
         issue(0, smem);
+        lddp(1);
         issue(1, smem + BUF);
         constexpr int OPS = GM == 2 ? 8 : 4;          // LDS-DMA instructions of one phase per wave
         const int rl = wn * 16 + (lane & 15);         // this lane's RHS row within a phase
@@ -1142,9 +1158,11 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 const double rcv[4] = {r01.x, r01.y, r23.x, r23.y};
                 float xs[4] = {x4.x, x4.y, x4.z, x4.w};
                 if (fx) {
-                    const bf16x4 hq = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.ldd + j);
-                    bf16x4 lq;
-                    if constexpr (DS == 2) lq = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.ldd + j);
+                    bf16x4 hq = dpre[nt & 1][mt], lq;
+                    if constexpr (DS == 2) {
+                        hq = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.ldd + j);
+                        lq = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.ldd + j);
+                    }
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         double dq = (double)(float)hq[r];
@@ -1166,6 +1184,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             panel_norms_wave(nrd, wm, K, rhs, sbx, sx, err, dmax);
             if (nt + 2 < 4) {
                 __syncthreads();                      // every wave is done with this phase's buffer
+                lddp(nt + 2);
                 issue(nt + 2, smem + (nt & 1) * BUF);
             }
         }

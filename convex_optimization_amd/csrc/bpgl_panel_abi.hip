@@ -36,7 +36,7 @@ struct bpgl_panel {
     int waves[2] = {0, 0};        // waves along the RHS per pass: 0 = 2 (8 waves), 4 = 16 waves ("waves" knobs)
     int dsplit = 1;               // bf16 pieces of the solver's direction (d_split knob; 1 since round 4)
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
-    int defer_x = 0;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; measured even)
+    int defer_x = 1;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; round 4 default)
     int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
     int carry_g = 1;              // carried gradient, one feature block ("carry_g" knob; ignored for nblock > 1)
     int64_t g_period = 64;        // exact gradient every g_period iterations ("g_refresh" knob)
