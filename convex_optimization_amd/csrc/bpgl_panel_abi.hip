@@ -32,7 +32,7 @@ struct bpgl_panel {
     std::vector<hipEvent_t> evs;
     int64_t timed_iters = 0;
     bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
-    int interleave[2] = {2, 1};   // mainloop variant per pass (tuning knobs; measured defaults)
+    int interleave[2] = {2, -1};  // mainloop variant per pass (tuning knobs; -1: the measured default, panel_ilv)
     int waves[2] = {0, 0};        // waves along the RHS per pass: 0 = 2 (8 waves), 4 = 16 waves ("waves" knobs)
     int dsplit = 1;               // bf16 pieces of the solver's direction (d_split knob; 1 since round 4)
     int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
@@ -107,9 +107,17 @@ int panel_launch_lo8_ilv(bpgl_panel* c, int which) {
     }
     return 0;
 }
+// the mainloop variant of a pass: the knob, or the measured default -- pass 1: 2 (software-pipelined);
+// pass 2: 2 with the bf16 direction alone at k >= 64 (+0.7 % at k = 64 and 128), else 1 (k = 32 and the
+// hi + lo direction; profiles/r04/ilv)
+int panel_ilv(const bpgl_panel* c, int which, int ns) {
+    const int v = c->interleave[which];
+    if (v >= 0) return v;
+    return which == 0 ? 2 : (ns == 1 && c->k >= 64 ? 2 : 1);
+}
 template <int NT, int NS>
 int panel_launch_lo8(bpgl_panel* c, int which) {
-    switch (c->interleave[which]) {
+    switch (panel_ilv(c, which, NS)) {
         case 0: return panel_launch_lo8_ilv<NT, NS, 0>(c, which);
         case 1: return panel_launch_lo8_ilv<NT, NS, 1>(c, which);
         default: return panel_launch_lo8_ilv<NT, NS, 2>(c, which);
@@ -159,7 +167,7 @@ int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int 
 }
 template <int NT, int NS, int WNX>
 int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    switch (c->interleave[which]) {
+    switch (panel_ilv(c, which, NS)) {
         case 0: return panel_launch_nt<NT, 0, NS, WNX>(c, which, fixed_block, out, mode);
         case 1: return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
         case 2: return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
@@ -663,8 +671,8 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
 
 int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) {
     if (!c || !key || !value) return fail(BPGL_E_ARG, "null argument");
-    if (!strcmp(key, "interleave1")) *value = c->interleave[0];
-    else if (!strcmp(key, "interleave2")) *value = c->interleave[1];
+    if (!strcmp(key, "interleave1")) *value = panel_ilv(c, 0, c->dsplit);
+    else if (!strcmp(key, "interleave2")) *value = panel_ilv(c, 1, c->dsplit);   // the solver's pass 2
     else if (!strcmp(key, "d_split")) *value = c->dsplit;
     else if (!strcmp(key, "waves1")) *value = c->waves[0];
     else if (!strcmp(key, "waves2")) *value = c->waves[1];

@@ -322,11 +322,12 @@ int bpgl_panel_set_kernel_timing(bpgl_panel* ctx, int enable);
 int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce (+ line search), step (0: folded into reduce), update */,
                             int64_t* samples);
 /* tuning knobs.  Results are bitwise independent of these: "interleave1",
- * "interleave2" (pass 1 / pass 2; "interleave" sets both) 0/1/2 -- LDS-DMA
+ * "interleave2" (pass 1 / pass 2; "interleave" sets both) 0/1/2/3 -- LDS-DMA
  * pieces issued together after each stage barrier (0), spread over the stage's
- * MFMA groups (1, pass-2 default), or spread and software-pipelined with
- * fragment reads one MFMA group ahead across the stage barrier (2, pass-1
- * default).
+ * MFMA groups (1), or spread and software-pipelined with fragment reads one MFMA
+ * group ahead across the stage barrier (2), or (3, k = 128) the staggered
+ * four-phase form.  Defaults: pass 1 -- 2; pass 2 -- 2 with the bf16 direction
+ * (d_split 1) at k >= 64, else 1 (round 4); get_tuning reports the form in use.
  * This one selects the solver's arithmetic (every choice is an exact line
  * search along the direction it takes): "d_split" 1 (default since ABI 200) --
  * the direction enters the A D pass as its bf16 rounding alone (half the
