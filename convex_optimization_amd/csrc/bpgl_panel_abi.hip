@@ -47,6 +47,7 @@ struct bpgl_panel {
     int64_t t_host = 0;           // iterations enqueued since the last reset
     int64_t last_refresh = 0;     // t_host of the last refresh
     int64_t n_refresh = 0;        // refreshes since the last reset
+    int64_t n_exact = 0;          // carried gradient: exact-gradient iterations since the last reset
     int64_t ldr() const { return m + op_pad; }
     int64_t ldd() const { return w + op_pad; }
 };
@@ -491,6 +492,7 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     c->t_host = 0;
     c->last_refresh = 0;
     c->n_refresh = 0;
+    c->n_exact = 0;
     p.err_iter = err_iter;
     p.rec_len = err_iter ? record_len : 0;
     HIP_TRY(hipMemsetAsync(p.cnt, 0, 8 * (int64_t)c->k, c->stream));   // arrival counters start at 0
@@ -545,6 +547,7 @@ int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
         const bool exact = panel_carry(c) && (c->t_host % c->g_period == 0 || c->last_refresh == c->t_host);
         if (!c->timing && c->gexec && i + kGraphIters <= n_iter && c->t_host % kGraphIters == 0) {
             HIP_TRY(hipGraphLaunch(exact ? c->gexec_ref : c->gexec, c->stream));
+            c->n_exact += exact;
             i += kGraphIters;
             c->t_host += kGraphIters;
         } else {
@@ -552,6 +555,7 @@ int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
                                     (refresh && (c->t_host + 1) % c->r_period == 0);
             if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0, exact, next_exact || i + 1 == n_iter)))
                 return rc;
+            c->n_exact += exact;
             if (c->timing) c->timed_iters++;
             ++i;
             ++c->t_host;
@@ -691,6 +695,7 @@ int bpgl_panel_stat(const bpgl_panel* c, const char* key, int64_t* value) {
     if (!c || !key || !value) return fail(BPGL_E_ARG, "null argument");
     if (!strcmp(key, "refreshes")) *value = c->n_refresh;
     else if (!strcmp(key, "iters_enqueued")) *value = c->t_host;
+    else if (!strcmp(key, "exact_gradients")) *value = c->n_exact;
     else return fail(BPGL_E_ARG, "unknown panel stat '%s'", key);
     return 0;
 }

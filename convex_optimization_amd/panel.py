@@ -207,7 +207,7 @@ class PanelLasso:
         return v.value
 
     def stat(self, key):
-        """Counter since the last reset: "refreshes", "iters_enqueued"."""
+        """Counter since the last reset: "refreshes", "iters_enqueued", "exact_gradients"."""
         v = ctypes.c_int64()
         N.check(_lib().bpgl_panel_stat(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_panel_stat")
         return v.value

@@ -357,13 +357,14 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * refresh -- the single-RHS path's carried gradient.  Measured at configs[4]: pass 1
  * 226 -> 196 us, and after 1000 iterations x within 4e-6 of the oracle instead of
  * 1.9e-5 (fp32 accumulation of small updates instead of re-reading R through its
- * 2^-17 pieces).  With it, lo8 bit 0 is not used (pass 1 multiplies S).
+ * 2^-17 pieces).  With it, lo8 bit 0 is not used (pass 1 multiplies V).
  * get_tuning("carry_g") reports the form in effect. */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_get_tuning(const bpgl_panel* ctx, const char* key, int64_t* value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
 /* Counters since the last reset: "refreshes" (exact residual refreshes run),
- * "iters_enqueued". */
+ * "iters_enqueued", "exact_gradients" (carried gradient: iterations whose pass 1
+ * computed G = A^T R exactly -- every g_refresh-th and the first after a refresh). */
 int bpgl_panel_stat(const bpgl_panel* ctx, const char* key, int64_t* value);
 /* The solver's fp64 residual R = A X - B, [nrhs][m] in device memory (valid after
  * the stream has drained). */

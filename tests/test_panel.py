@@ -318,6 +318,8 @@ def test_panel_lo8_graph_equals_eager(carry):
     pl.set_tuning("r_refresh", 16)
     a = pl.run(B, mu, 44, use_graph=True)["x"]
     assert pl.stat("refreshes") == 2
+    # with the carried gradient (g_refresh 64): iteration 0, and the first after each refresh (16, 32)
+    assert pl.stat("exact_gradients") == (3 if carry else 0)
     b = pl.run(B, mu, 44, use_graph=False)["x"]
     np.testing.assert_array_equal(a, b)
     pl.solver_reset(B, mu)                      # split step calls: the schedule follows the iteration count
@@ -415,6 +417,7 @@ def test_panel_carried_gradient_graph_equals_eager():
     for n_it in (5, 3, 16, 9, 11):
         pl.solver_step(n_it)
     np.testing.assert_array_equal(pl.solver_x(), a)
+    assert pl.stat("exact_gradients") == 3          # iterations 0, 16 and 32 of 44
     pl.solver_reset(B, mu)
     prev = [objective(Ab, B[:, j], mu[j], np.zeros(1024)) for j in range(128)]
     for _ in range(6):
