@@ -735,7 +735,8 @@ def main_panel(args):
         "vs_baseline": None,
         "dtype": "bf16 (A) x hi+lo bf16 residual x " + ("hi+lo bf16" if d_split == 2 else "bf16") +
                  " direction, fp32 MFMA accumulate, fp64 reduce" +
-                 (f"; gradient carried in fp32 (G += gamma A^T bf16 S), exact every {g_period}" if carry else ""),
+                 (f"; gradient carried in fp32 (G += A^T bf16(V), V = gamma S + the previous rounding), exact every "
+                  f"{g_period}" if carry else ""),
         "data": "synthetic (A ~ N(0,1) rows unit-norm, bf16 in HBM; X_true density 0.4; B = A X_true + 0.01 E)",
         "config": {
             "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
@@ -757,7 +758,7 @@ def main_panel(args):
             "kernel_avg_ms": kms, "status": st,
         },
         "roofline": {
-            "bound": "hbm", "kernel": {"pass1_mfma": "k_panel_pass1 (A^T R panel GEMM + shrink)",
+            "bound": "hbm", "kernel": {"pass1_mfma": "k_panel_pass1 (A^T V (carried) / A^T R (exact) panel GEMM + shrink)",
                                        "pass2_mfma": "k_panel_pass2 (A D panel GEMM)"}[dom],
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": pmc_traffic(f"panel_m{m}_n{n}_k{k}", {"pass1_mfma": "k_panel_pass1",
