@@ -44,9 +44,18 @@ ms_per_step come from the median window, with the one-pass exact-gradient refres
 time minus the refreshes it happened to contain, plus K/256 refreshes, each at the
 event-timed refresh cost.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
-Rank 0 prints one JSON line.
+N = 1 side legs (the same JSON line, each with its own ms_per_step, roofline and
+kernel averages; a leg that fails records {"error": ...}): "config3" (configs[3],
+1048576 x 4096 fp32), "config4" (configs[4], k = 128 right-hand sides on bf16 A,
+the MFMA panel path) and "config2_one_gpu" (configs[2]'s whole 8192 x 524288
+matrix on this one GPU).  --no-side-legs skips them.
+
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N > 1 under
+torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE env) the
+ranks run directly; without it (WORLD_SIZE unset) this process touches no GPU,
+starts `python -m torch.distributed.run --nproc-per-node N bench.py <same args>`
+as a child, relays its output and exits with its status.  Rank 0 prints one
+JSON line.
 """
 import argparse
 import json
@@ -115,6 +124,8 @@ def parse():
                     help="N > 1: value = weak scaling (m=8192, n=65536 N, block-iters/s) instead of the default "
                          "strong scaling of the metric's 8192 x 65536 matrix")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-side-legs", action="store_true",
+                    help="N = 1: skip the config3 / config4 / config2_one_gpu legs of the default line")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=20190325)
     ap.add_argument("--fused", type=int, default=0, help="1: two-launch fused iteration; 0 (default): five kernels")
@@ -654,8 +665,11 @@ def panel_fill_bytes(m, w, k, which, d_split=2, r_pieces=2):
 
 
 def main_panel(args):
-    """configs[4]: k right-hand sides on m x n bf16 A (PanelLasso, MFMA passes)."""
-    import numpy as np
+    emit(measure_panel(args))
+
+
+def measure_panel(args):
+    """configs[4]: k right-hand sides on m x n bf16 A (PanelLasso, MFMA passes); the JSON line."""
     import torch
     from convex_optimization_amd.panel import PanelLasso
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -782,7 +796,7 @@ def main_panel(args):
                          "frac": fill_bytes / (kms[dom] * 1e-3) / 1e9 / LDS_FILL_CAP_GBS},
         },
     }
-    emit(out)
+    return out
 
 
 _JSON_OUT = None
@@ -803,8 +817,157 @@ def emit(out):
     (_JSON_OUT or sys.stdout).flush()
 
 
+def release():
+    """drop the previous measurement's context, A and graphs before the next one"""
+    import gc as _gc
+    _gc.collect()
+    try:
+        import torch
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    except Exception:
+        pass
+
+
+def side_legs_apply(args):
+    """the N = 1 side legs ride on the default line only (configs[1], one block, fp32, no comm)"""
+    return (not args.no_side_legs and args.config in (None, 1) and args.block == 1 and args.type == "float"
+            and not args.comm and args.rhs == 1 and (args.m, args.n_per_gpu) == (M, N_PER_GPU))
+
+
+def single_leg(ctx, args, m, n, label, steps_cap=None, ramp_cap=None):
+    """one single-GPU measurement (measure()) summarised like the value line: value, ms_per_step,
+    roofline (the dominant kernel's and the iteration's fractions) and the kernel averages"""
+    a2 = argparse.Namespace(**vars(args))
+    a2.m, a2.n_per_gpu, a2.comm = m, n, False
+    if steps_cap:
+        a2.steps = min(a2.steps, steps_cap)
+    if ramp_cap:
+        a2.ramp = min(a2.ramp, ramp_cap)
+    res = measure(ctx, a2, m, n)
+    K = a2.steps
+    v, raw = window_rate(res, K)
+    kms = res["kernel_ms"]
+    ml, w = res["m_local"], res["w_local"]
+    if kms.get("onepass", 0.0) > 0:
+        dom, kname = "onepass", "k_onepass"
+        dom_bytes, it_bytes = alg_bytes_onepass(ml, w), alg_bytes_iter_onepass(ml, w)
+    else:
+        dom = max(("colpass", "rowpass"), key=lambda q: kms[q])
+        kname = "k_" + dom
+        dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(ml, w)
+        it_bytes = alg_bytes_iter(ml, w)
+    ms = 1e3 / v
+    achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
+    traffic = pmc_traffic(f"m{m}_n{n}_b1_float_g1", kname)
+    return {"workload": label, "value": v, "unit": "iters/s", "steps": K, "warmup": a2.warmup,
+            "ms_per_step": ms, "ms_per_step_raw_median": raw * 1e3,
+            "iteration": "one pass over A" if dom == "onepass" else "two passes over A",
+            "windows": res["windows"], "refresh": {"period": res["refresh_period"], "ms_per_refresh": res["refresh_ms"]},
+            "onepass_fallbacks": res["fallbacks"], "measure_attempts": res["attempts"],
+            "kernel_avg_ms": kms, "status": res["status"],
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "alg_bytes_per_launch": dom_bytes,
+                         "avg_launch_ms": kms[dom], "traffic": traffic,
+                         "iteration_frac_end_to_end": it_bytes / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
+                         "survey_two_pass_frac": alg_bytes_iter(ml, w) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9)}}
+
+
+def panel_leg(args):
+    """configs[4] through measure_panel, summarised for the N = 1 line"""
+    a2 = argparse.Namespace(**vars(args))
+    a2.config, a2.rhs, a2.m, a2.n_per_gpu = 4, 128, M, N_PER_GPU
+    p = measure_panel(a2)
+    c = p["config"]
+    return {"workload": c["workload"], "value": p["value"], "unit": p["unit"], "steps": p["steps"],
+            "warmup": p["warmup"], "ms_per_step": p["ms_per_step"], "dtype": p["dtype"],
+            "rhs_iters_per_s": c["rhs_iters_per_s"], "iter_roofline_frac": c["iter_roofline_frac"],
+            "hbm_roofline_iters_per_s": c["hbm_roofline_iters_per_s"], "windows_s": c["windows_s"],
+            "kernel_avg_ms": c["kernel_avg_ms"], "status": c["status"],
+            "tuning": {q: c[q] for q in ("d_split", "carry_g", "g_refresh", "defer_x", "kchunks", "interleave12")},
+            "roofline": p["roofline"]}
+
+
+def side_legs(ctx, args, out):
+    """N = 1: configs[3], configs[4] and configs[2]'s whole matrix on this GPU, each on the driver's
+    clock beside the value line (its own windows of --steps iterations, capped for the 2.7 ms
+    iterations of configs[3] / [2]); a leg that raises records {"error": ...}"""
+    legs = (("config3", lambda: single_leg(ctx, args, 1048576, 4096,
+                                           "configs[3]: m=1048576 n=4096 float A, 1 feature block, 1 GPU",
+                                           steps_cap=64, ramp_cap=128)),
+            ("config4", lambda: panel_leg(args)),
+            ("config2_one_gpu", lambda: single_leg(ctx, args, 8192, 524288,
+                                                   "configs[2]'s whole matrix on one GPU: m=8192 n=524288 float A, "
+                                                   "1 feature block", steps_cap=64, ramp_cap=128)))
+    for key, run in legs:
+        progress(f"side leg {key}")
+        try:
+            release()
+            out[key] = run()
+        except Exception as e:
+            out[key] = {"error": f"{type(e).__name__}: {e}"[:400]}
+        release()
+
+
+def visible_gpu_count():
+    """GPUs a child process would see, counted in a separate interpreter so that this one never
+    loads HIP (torch.cuda.device_count() does not initialise the GPU on this image, but the
+    launcher does not rely on that)."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except Exception:
+        return 0
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(cmd):
+    """the rank launcher as a child process: its stdout / stderr are this process's (relayed as
+    written), its exit status returned"""
+    import subprocess
+    return subprocess.call(cmd)
+
+
+def needs_launch(args, env=None):
+    """--gpus N > 1 outside torch.distributed.run (no WORLD_SIZE): this process launches the ranks"""
+    return args.gpus > 1 and "WORLD_SIZE" not in (os.environ if env is None else env)
+
+
+def launch_ranks(args, argv, spawn=None, count=None):
+    """`python3 bench.py --gpus N` (N > 1) outside torch.distributed.run: start
+    `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+    --master-port P bench.py <argv>` as a fresh child process (no exec: this process never touches
+    the GPU) and return its exit status (128 + signal for a signalled child).  N above the visible
+    GPU count fails at once with status 2, unless BPGL_BENCH_DEVICE puts every rank on one GPU
+    (the rehearsal mode of Ctx)."""
+    n = args.gpus
+    if not os.environ.get("BPGL_BENCH_DEVICE"):
+        have = (count or visible_gpu_count)()
+        if have < n:
+            sys.stderr.write(f"bench.py: --gpus {n} but only {have} GPU(s) visible; nothing launched\n")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "bench.py")] + list(argv)
+    progress(f"launching {n} ranks: {' '.join(cmd)}")
+    sys.stdout.flush()
+    sys.stderr.flush()
+    rc = (spawn or _spawn)(cmd)
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     args = parse()
+    if needs_launch(args):
+        # before quiet_stdout (the child inherits fd 1 for its JSON line) and before torch
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     quiet_stdout()
     rank = int(os.environ.get("RANK", "0"))
     cores, cpu_info = host_cores()
@@ -995,7 +1158,7 @@ def main():
                     res = measure(solo, a3, m, args.n_per_gpu)
                     n1 = window_rate(res, K)[0]
                     o = leg_summary(solo, res, K, 1, False)
-                except BaseException as e:   # noqa: B036 -- never skip the barrier
+                except Exception as e:   # recorded; the barrier below is still reached
                     out["n1_same_run"] = {"error": f"{type(e).__name__}: {e}"[:400]}
             ctx.barrier()
             if ctx.rank == 0 and n1:
@@ -1005,6 +1168,9 @@ def main():
     if G == 1 and args.type == "float" and res is not None:
         out["config"]["vendor_gemv_yardstick"] = vendor_yardstick(res["gc"])
         out["config"]["vendor_iteration_yardstick"] = vendor_iteration_yardstick(res["gc"], res["b"], res["mu"])
+    if G == 1 and side_legs_apply(args):
+        res = None
+        side_legs(ctx, args, out)
     if ctx.rank == 0:
         emit(out)
     if ctx.world > 1:

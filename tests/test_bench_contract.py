@@ -222,3 +222,74 @@ def test_measure_error_is_an_exception():
     """a side leg whose windows are all invalid must be recorded, not end the run"""
     b = _bench()
     assert issubclass(b.MeasureError, Exception)
+
+
+_LAUNCH_SCRIPT = r'''
+import importlib.util, json, os, sys
+root = sys.argv[1]
+rc_child, have = int(sys.argv[2]), int(sys.argv[3])
+sys.argv = ["bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5"]
+spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+b = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(b)
+calls = []
+b._spawn = lambda cmd: (calls.append(cmd), rc_child)[1]
+b.visible_gpu_count = lambda: have
+rc = None
+try:
+    b.main()
+except SystemExit as e:
+    rc = e.code
+print(json.dumps({"rc": rc, "cmd": calls, "torch": "torch" in sys.modules,
+                  "hip": [m for m in sys.modules if m.startswith("torch.cuda")]}))
+'''
+
+
+def _run_launcher(rc_child, have, extra_env=None):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "BPGL_BENCH_DEVICE")}
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, "-c", _LAUNCH_SCRIPT, ROOT, str(rc_child), str(have)],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_launcher_starts_ranks_as_a_child_without_touching_the_gpu():
+    """`python3 bench.py --gpus 2` with no WORLD_SIZE (VERDICT r04 Missing #1): the parent starts
+    torch.distributed.run as a child with the same arguments, never imports torch, and exits with
+    the child's status"""
+    o = _run_launcher(0, 8)
+    assert o["rc"] == 0 and not o["torch"] and not o["hip"]
+    (cmd,) = o["cmd"]
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 1] == "-m" and "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert "--nnodes=1" in cmd and any(c.startswith("--master-port=") for c in cmd)
+    j = [k for k, c in enumerate(cmd) if c.endswith("bench.py")][-1]
+    assert cmd[j + 1:] == ["--gpus", "2", "--steps", "20", "--warmup", "5"]
+    assert _run_launcher(3, 8)["rc"] == 3          # the child's status is propagated
+    assert _run_launcher(-9, 8)["rc"] == 137       # a signalled child: 128 + signal
+
+
+def test_launcher_fails_fast_without_enough_gpus():
+    o = _run_launcher(0, 1)
+    assert o["rc"] == 2 and o["cmd"] == [] and not o["torch"]
+    # the one-GPU rehearsal (every rank on BPGL_BENCH_DEVICE) skips the count
+    o = _run_launcher(0, 1, {"BPGL_BENCH_DEVICE": "0"})
+    assert o["rc"] == 0 and len(o["cmd"]) == 1
+
+
+def test_launch_decision():
+    b = _bench()
+    a = _parse(b, ["--gpus", "2"])
+    assert b.needs_launch(a, {}) and not b.needs_launch(a, {"WORLD_SIZE": "2"})
+    assert not b.needs_launch(_parse(b, []), {})
+
+
+def test_side_legs_ride_on_the_default_line_only():
+    b = _bench()
+    assert b.side_legs_apply(_parse(b, []))
+    for argv in (["--no-side-legs"], ["--config", "3"], ["--type", "bf16"], ["--block", "2"], ["--comm"]):
+        assert not b.side_legs_apply(_parse(b, argv)), argv
