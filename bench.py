@@ -128,14 +128,10 @@ def parse():
                     help="N = 1: skip the config3 / config4 / config2_one_gpu legs of the default line")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=20190325)
-    ap.add_argument("--fused", type=int, default=0, help="1: two-launch fused iteration; 0 (default): five kernels")
     ap.add_argument("--onepass", type=int, default=-1, choices=[-1, 0, 1],
                     help="one pass over A per iteration: -1 (default) when eligible (1 block, 1 rank), 0 off, 1 required")
     ap.add_argument("--tail-row-blocks", type=int, default=-1, choices=[-1, 0, 1],
                     help="one-pass tail: residual update on blocks of its own (1, library default) or first in every block (0)")
-    ap.add_argument("--onepass-variant", type=int, default=0, help="one-pass ring depth / prefetch variant (0-3)")
-    ap.add_argument("--onepass-fold", type=int, default=-1, choices=[-1, 0, 1],
-                    help="one-pass U fold inside k_onepass (1) or in k_onepass_fold / the tail (0, library default)")
     ap.add_argument("--graph-max", type=int, default=-1,
                     help="largest hipGraph of iterations replayed (power of two; -1: library default, 64)")
     ap.add_argument("--onepass-cache", type=int, default=-1,
@@ -153,28 +149,12 @@ def parse():
                     help="k > 1: configs[4] panel path (k right-hand sides, bf16 A, MFMA), 1 GPU")
     ap.add_argument("--kchunks", type=int, default=0, help="panel path split-K chunks (0 = auto)")
     ap.add_argument("--interleave", type=int, default=-1,
-                    help="panel path mainloop variant 0/1/2/3 for both passes (-1: library defaults)")
+                    help="panel path mainloop variant 0/1/2 for both passes (-1: library defaults)")
     ap.add_argument("--interleave1", type=int, default=-1, help="panel path pass-1 mainloop variant (-1: default)")
     ap.add_argument("--interleave2", type=int, default=-1, help="panel path pass-2 mainloop variant (-1: default)")
     ap.add_argument("--d-split", type=int, default=-1, choices=[-1, 1, 2],
                     help="panel path: the direction enters the A D pass as a hi + lo bf16 pair (2) or as its "
                          "bf16 rounding (1); -1: library default")
-    ap.add_argument("--waves1", type=int, default=-1, choices=[-1, 0, 4],
-                    help="panel path, pass 1: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
-    ap.add_argument("--waves2", type=int, default=-1, choices=[-1, 0, 4],
-                    help="panel path, pass 2: waves along the RHS (0: 8 waves per block, 4: 16 waves; -1 default)")
-    ap.add_argument("--write-through", type=int, default=-1,
-                    help="panel path: write-through store sites mask (1 pass-1 epilogue, 2 pass-2 slab, 4 S, "
-                         "8 R; -1: library default)")
-    ap.add_argument("--op-pad", type=int, default=0,
-                    help="panel path: bf16 elements appended to each RHS row of the operand images (multiple of 64)")
-    ap.add_argument("--lda-pad", type=int, default=0, help="panel path: columns appended to each row of bf16 A")
-    ap.add_argument("--lo8", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
-                    help="panel path: e4m3 lo products, bit 0 pass 1 (residual), bit 1 pass 2 (direction); "
-                         "-1: library default")
-    ap.add_argument("--r-refresh", type=int, default=-1,
-                    help="panel path with lo8 in pass 2: exact residual refresh period (multiple of 8; 0 never; "
-                         "-1: library default)")
     ap.add_argument("--carry-g", type=int, default=-1, choices=[-1, 0, 1],
                     help="panel path, one block: carry G += gamma A^T S (one bf16 product in pass 1) between exact "
                          "hi+lo gradients (1); -1: library default")
@@ -347,17 +327,13 @@ def measure(ctx, args, m, n_total):
     import torch
     progress(f"measure m={m} n={n_total} shard={args.shard} exchange_fp32={args.exchange_fp32}: building the instance")
     gc, b, mu = build_problem(ctx, m, n_total, args.block, args.type, args.seed, args.comm, args.shard)
-    gc.set_tuning("fused", args.fused)
     gc.set_tuning("onepass", args.onepass)
     if args.exchange_fp32:
         gc.set_tuning("exchange_fp32", -1)
-    gc.set_tuning("onepass_variant", args.onepass_variant)
     if args.tail_row_blocks >= 0:
         gc.set_tuning("tail_row_blocks", args.tail_row_blocks)
     if args.onepass_cache >= 0:
         gc.set_tuning("onepass_cache_permille", args.onepass_cache)
-    if args.onepass_fold >= 0:
-        gc.set_tuning("onepass_fold", args.onepass_fold)
     if args.graph_max > 0:
         gc.set_tuning("graph_max", args.graph_max)
 
@@ -680,7 +656,7 @@ def measure_panel(args):
     A = torch.randn(m, n, device="cuda", generator=g)
     A /= A.norm(dim=1, keepdim=True)
     Xt = torch.randn(n, k, device="cuda", generator=g) * (torch.rand(n, k, device="cuda", generator=g) < 0.4)
-    pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks, op_pad=args.op_pad, lda_pad=args.lda_pad)
+    pl = PanelLasso(A, args.block, nrhs=k, device=0, kchunks=args.kchunks)
     if args.interleave >= 0:
         pl.set_tuning("interleave", args.interleave)
     for q in (1, 2):
@@ -690,19 +666,10 @@ def measure_panel(args):
         pl.set_tuning("d_split", args.d_split)
     if args.defer_x >= 0:
         pl.set_tuning("defer_x", args.defer_x)
-    if args.write_through >= 0:
-        pl.set_tuning("write_through", args.write_through)
-    if args.lo8 >= 0:
-        pl.set_tuning("lo8", args.lo8)
-    if args.r_refresh >= 0:
-        pl.set_tuning("r_refresh", args.r_refresh)
     if args.carry_g >= 0:
         pl.set_tuning("carry_g", args.carry_g)
     if args.g_refresh >= 0:
         pl.set_tuning("g_refresh", args.g_refresh)
-    for q in (1, 2):
-        if getattr(args, f"waves{q}") >= 0:
-            pl.set_tuning(f"waves{q}", getattr(args, f"waves{q}"))
     d_split = pl.get_tuning("d_split")
     carry, g_period = pl.get_tuning("carry_g"), pl.get_tuning("g_refresh")
     del A
@@ -755,11 +722,8 @@ def measure_panel(args):
         "config": {
             "workload": f"configs[4]: k={k} right-hand sides, m={m} n={n} bf16 A, {args.block} feature block(s), 1 GPU",
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
-            "interleave": args.interleave, "d_split": d_split, "write_through": pl.get_tuning("write_through"),
-            "waves": [pl.get_tuning("waves1"), pl.get_tuning("waves2")],
-            "defer_x": pl.get_tuning("defer_x"), "op_pad": pl.get_tuning("op_pad"), "lda_pad": args.lda_pad,
-            "lo8": pl.get_tuning("lo8"), "r_refresh": pl.get_tuning("r_refresh"), "refreshes": pl.stat("refreshes"),
-            "carry_g": carry, "g_refresh": g_period,
+            "interleave": args.interleave, "d_split": d_split, "defer_x": pl.get_tuning("defer_x"),
+            "carry_g": carry, "g_refresh": g_period, "exact_gradients": pl.stat("exact_gradients"),
             "interleave12": [pl.get_tuning("interleave1"), pl.get_tuning("interleave2")],
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
@@ -999,8 +963,7 @@ def main():
     else:
         dom = max(("colpass", "rowpass"), key=lambda k: kms[k])
         dom_bytes = (alg_bytes_colpass if dom == "colpass" else alg_bytes_rowpass)(ml, w, sa)
-        kname = {("colpass", 1): "k_iter_a", ("rowpass", 1): "k_iter_b",
-                 ("colpass", 0): "k_colpass", ("rowpass", 0): "k_rowpass"}[(dom, int(args.fused))]
+        kname = "k_" + dom
         it_bytes = alg_bytes_iter(ml, w, sa)
     two_pass_bytes = alg_bytes_iter(ml, w, sa)
     achieved = dom_bytes / (kms[dom] * 1e-3) / 1e9
@@ -1053,7 +1016,6 @@ def main():
             "refresh": {"period": res["refresh_period"], "ms_per_refresh": res["refresh_ms"],
                         "folded": "window time - refreshes inside x ms_per_refresh + K/period x ms_per_refresh"},
             "onepass_fallbacks": res["fallbacks"],
-            "fused": args.fused,
             "iters_per_s_eager_with_events": iters_s_ev,
             "kernel_avg_ms": kms,
             "allreduce_ms_per_rank": allreduce_ms,
@@ -1061,9 +1023,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": kname + ({"k_iter_a": " (A^T s11 pass + segment-finisher shrink)",
-                                "k_iter_b": " (A D pass + row-chunk finishers + line search)",
-                                "k_colpass": " (A^T s11 pass)", "k_rowpass": " (A D pass)",
+            "kernel": kname + ({"k_colpass": " (A^T s11 pass)", "k_rowpass": " (A D pass)",
                                 "k_onepass": " (A D and A^T (A D) in one pass over A)"}[kname]),
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,

@@ -20,7 +20,6 @@
 #include "../../include/bpgl.h"
 #include "bpgl_host.h"
 #include "bpgl_kernels.h"
-#include "bpgl_fused.h"
 #include "bpgl_onepass.h"
 
 using namespace bpgl;
@@ -102,7 +101,6 @@ struct bpgl_ctx {
     bool kind_used[kTimedKinds] = {};
     double wall_tick_s = 1e-8;
     int reverse_rows = 0;
-    int fused = 0;
     int col_mode = 1;      // k_colpass row schedule (see launch_colpass)
     int nt_loads = 1;
     int tail_permille = 120;
@@ -117,17 +115,12 @@ struct bpgl_ctx {
     // 3e-15 (profiles/r01/sweeps/onepass_refresh_drift.jsonl); 256 keeps the refresh (one A^T r pass)
     // at 0.4 % of the iteration time
     int op_refresh = 256;
-    int op_variant = 0;        // ring depth / prefetch variant (OpVar)
     // permille of each row group read with cache-allocating loads (-1: auto, op_cache_auto)
     int op_cache = -1;
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
     int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
     int op_rowb = 1;   // k_onepass_tail: residual update on blocks of its own ("tail_row_blocks" knob)
-    // fold the U partials inside k_onepass ("onepass_fold" 1) or in k_onepass_fold / the tail (0, default:
-    // the in-kernel form's write-through partials and segment barrier cost more than the launch it
-    // saves -- m = 1024 rows: k_onepass 55.0 -> 67.9 us against a 12.4 us fold; profiles/r03/fold_sweep_v1)
-    int op_fold = 0;
     // row shards (bpgl_set_shard): A holds this rank's rows of the single feature block; x, D, g
     // are replicated and each one-pass iteration all-reduces [U | r.s23 | s23.s23]
     bool rows = false;
@@ -203,8 +196,7 @@ int op_cache_eff(const bpgl_ctx* c) {
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, Dbuf, cnt, opG, opUs, opPG, opS, opABE,
-        opSeg, opUsum, total;
+    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, opG, opUs, opPG, opS, opABE, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -216,8 +208,6 @@ Layout layout(const bpgl_ctx* c) {
     L.D = k.take(8 * c->wp);
     L.parts = k.take(8 * 4 * (int64_t)std::max(c->nparts, c->op_tail_grid));
     L.parts2 = k.take(8 * 2 * std::max<int64_t>(kMaxReduceBlocks, c->nchunk));
-    L.Dbuf = k.take(8 * 2 * c->wp);
-    L.cnt = k.take(8 * ((int64_t)c->nseg + c->nchunk));
     // column shards exchange [s23 (m) | 2 | err slots]; row shards [U (wp) | r.s23 | s23.s23 | failed]
     L.comm = k.take(8 * std::max<int64_t>(c->m + 2 + kMaxRanks, c->wp + 3));
     L.r = k.take(8 * c->m);
@@ -230,8 +220,6 @@ Layout layout(const bpgl_ctx* c) {
     L.opPG = k.take(op ? 8 * c->m * c->op_SB : 0);
     L.opS = k.take(op && c->rows ? 8 * c->m : 0);
     L.opABE = k.take(op && c->rows ? 8 * 4 : 0);
-    L.opSeg = k.take(op ? 8 * (int64_t)c->op_SB : 0);
-    L.opUsum = k.take(op && !c->rows ? 8 * c->wp : 0);
     L.total = k.off;
     return L;
 }
@@ -285,27 +273,6 @@ int rowpass(bpgl_ctx* c, const double* d, double* slab, int fixed_block) {
     }
 }
 
-template <typename T>
-int launch_iter(bpgl_ctx* c, int which) {
-    if (which == 0) {
-        if (c->nt_loads) hipLaunchKernelGGL((k_iter_a<T, true>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
-        else hipLaunchKernelGGL((k_iter_a<T, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
-        LAUNCH_CHECK("k_iter_a");
-    } else {
-        if (c->nt_loads) hipLaunchKernelGGL((k_iter_b<T, true>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
-        else hipLaunchKernelGGL((k_iter_b<T, false>), grid_tiles(c), dim3(kThreads), 0, c->stream, c->p);
-        LAUNCH_CHECK("k_iter_b");
-    }
-    return 0;
-}
-int iter_kernel(bpgl_ctx* c, int which) {
-    switch (c->dtype) {
-        case BPGL_F32: return launch_iter<float>(c, which);
-        case BPGL_F64: return launch_iter<double>(c, which);
-        default: return launch_iter<bf16_t>(c, which);
-    }
-}
-
 unsigned rowreduce_blocks(const bpgl_ctx* c) {
     return (unsigned)std::min<int64_t>(cdiv(c->m, kRowsPerReduce), kMaxReduceBlocks);
 }
@@ -328,24 +295,19 @@ int rowreduce(bpgl_ctx* c, const double* slab, double* out, int mode) { return r
 // ---------------------------------------------------------------------------
 // one-pass iteration (bpgl_onepass.h)
 // ---------------------------------------------------------------------------
-// ring slots NB and rows in flight PF per variant (tuning key "onepass_variant"); the loads
-// per lane and row (LU: 4 KiB of fp32 / fp64, 3 KiB of bf16 A per wave and row) are fixed per
-// storage type because they set the geometry.  bf16 takes LU 3: its per-row instruction path
-// (the same 16-24 fp64 FMAs and wave sums as fp32) limits it at LU 2 (2.9k it/s), LU 4 spills;
+// ring slots NB and rows in flight PF per storage type; the loads per lane and row (LU: 4 KiB of
+// fp32 / fp64, 3 KiB of bf16 A per wave and row) set the geometry.  Round 4 re-measured the deeper
+// and shallower rings (NB 14-18, PF 3-4; bf16 NB 9-11) at 1024 x 65536 and 8192 x 65536: the
+// defaults stayed best (61.6-81.5 us against 60.6 us per strong N = 8 shard,
+// profiles/r04/split_model/variants_m1024); the variants were removed in round 5.  bf16 takes LU 3:
+// its per-row instruction path (the same 16-24 fp64 FMAs and wave sums as fp32) limits it at LU 2
+// (2.9k it/s), LU 4 spills;
 // LU 3 with a 12-row ring reaches 3.4-3.5k it/s at configs[1]'s shape.
 // profiles/r01/sweeps/onepass6_probe.jsonl, onepass_bf16_lu3_variants.jsonl
 template <typename T> struct OpLU { static constexpr int LU = 4; };
 template <> struct OpLU<bf16_t> { static constexpr int LU = 3; };
-template <typename T, int V> struct OpVar;
-template <typename T> struct OpVar<T, 0> { static constexpr int NB = 16, PF = 3; };
-template <typename T> struct OpVar<T, 1> { static constexpr int NB = 18, PF = 4; };
-template <typename T> struct OpVar<T, 2> { static constexpr int NB = 14, PF = 3; };
-template <typename T> struct OpVar<T, 3> { static constexpr int NB = 17, PF = 4; };
-template <> struct OpVar<bf16_t, 0> { static constexpr int NB = 12, PF = 2; };
-template <> struct OpVar<bf16_t, 1> { static constexpr int NB = 10, PF = 2; };
-template <> struct OpVar<bf16_t, 2> { static constexpr int NB = 11, PF = 2; };
-template <> struct OpVar<bf16_t, 3> { static constexpr int NB = 9, PF = 2; };
-constexpr int kOpVariants = 4;
+template <typename T> struct OpRing { static constexpr int NB = 16, PF = 3; };
+template <> struct OpRing<bf16_t> { static constexpr int NB = 12, PF = 2; };
 
 // the two-pass kernels' view of one-pass state: g is read from G (one slab row), s23 from S
 Params op_params(const bpgl_ctx* c) {
@@ -357,36 +319,18 @@ Params op_params(const bpgl_ctx* c) {
     return q;
 }
 // GPL: granules per lane of the row hand-off (SB <= 64: 1, SB <= 128: 2)
-template <typename T, int V, int GPL>
-const void* onepass_fn_v() { return (const void*)k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU, GPL>; }
 template <typename T, int GPL>
-const void* onepass_fn_g(int v) {
-    switch (v) {
-        case 1: return onepass_fn_v<T, 1, GPL>();
-        case 2: return onepass_fn_v<T, 2, GPL>();
-        case 3: return onepass_fn_v<T, 3, GPL>();
-        default: return onepass_fn_v<T, 0, GPL>();
-    }
-}
+const void* onepass_fn_g() { return (const void*)k_onepass<T, OpRing<T>::NB, OpRing<T>::PF, OpLU<T>::LU, GPL>; }
 template <typename T>
-const void* onepass_fn_t(int v, int gpl) { return gpl == 2 ? onepass_fn_g<T, 2>(v) : onepass_fn_g<T, 1>(v); }
-const void* onepass_fn(int dtype, int v, int gpl) {
-    return dtype == BPGL_F32 ? onepass_fn_t<float>(v, gpl)
-         : dtype == BPGL_F64 ? onepass_fn_t<double>(v, gpl) : onepass_fn_t<bf16_t>(v, gpl);
-}
-template <typename T, int V, int GPL>
-void onepass_launch_v(bpgl_ctx* c) {
-    hipLaunchKernelGGL((k_onepass<T, OpVar<T, V>::NB, OpVar<T, V>::PF, OpLU<T>::LU, GPL>),
-                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, op_params(c), c->op);
+const void* onepass_fn_t(int gpl) { return gpl == 2 ? onepass_fn_g<T, 2>() : onepass_fn_g<T, 1>(); }
+const void* onepass_fn(int dtype, int gpl) {
+    return dtype == BPGL_F32 ? onepass_fn_t<float>(gpl) : dtype == BPGL_F64 ? onepass_fn_t<double>(gpl)
+                                                                             : onepass_fn_t<bf16_t>(gpl);
 }
 template <typename T, int GPL>
 void onepass_launch_g(bpgl_ctx* c) {
-    switch (c->op_variant) {
-        case 1: onepass_launch_v<T, 1, GPL>(c); break;
-        case 2: onepass_launch_v<T, 2, GPL>(c); break;
-        case 3: onepass_launch_v<T, 3, GPL>(c); break;
-        default: onepass_launch_v<T, 0, GPL>(c); break;
-    }
+    hipLaunchKernelGGL((k_onepass<T, OpRing<T>::NB, OpRing<T>::PF, OpLU<T>::LU, GPL>),
+                       dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, op_params(c), c->op);
 }
 template <typename T>
 void onepass_launch_t(bpgl_ctx* c) {
@@ -419,20 +363,10 @@ OnePassArgs op_tail_args(const bpgl_ctx* c) {
         o.Us = c->p.comm;
         o.ngroups = 1;
         if (xch_f32(c)) o.Uf = reinterpret_cast<const float*>(c->p.comm);
-    } else if (c->op.fold) {   // one rank: k_onepass folded U already
-        o.Us = c->op.Ufold;
-        o.ngroups = 1;
     } else {
         o.tailw = c->op_ngroups <= kOpTailWaveGroups ? 1 : 0;
     }
     return o;
-}
-// the per-solve part of the one-pass arguments (after op_on is known): the in-kernel fold
-void op_configure(bpgl_ctx* c) {
-    if (!c->op_shape) return;
-    c->op.fold = c->op_on && c->op_fold ? 1 : 0;
-    c->op.rows_out = c->rows && c->op.fold ? 1 : 0;
-    c->op.Ufold32 = c->op.fold && xch_f32(c) ? reinterpret_cast<float*>(c->p.comm) : nullptr;
 }
 template <bool UPDATE>
 int onepass_tail(bpgl_ctx* c) {
@@ -470,9 +404,8 @@ const char* onepass_ineligible(bpgl_ctx* c) {
     if (!c->op_shape) return "needs one feature block and at most 128 segment blocks per row";
     if (!c->rows && (c->nranks != 1 || c->comm || c->external))
         return "column shards need a single rank without a communicator (row shards run it on several)";
-    if (c->fused) return "not combined with the fused iteration";
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_variant, c->op_gpl), kThreads, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_gpl), kThreads, 0) != hipSuccess || nb < 1)
         return "kernel does not fit on a CU";
     if ((int64_t)c->op_ngroups * c->op_SB > (int64_t)nb * c->cus) return "grid exceeds the resident capacity";
     return nullptr;
@@ -511,48 +444,6 @@ void ev_record(bpgl_ctx* c, int64_t it, int kind, int end) {
     c->kind_used[kind] = true;
 }
 
-// Fused iteration (tuning key "fused"): phase 0 = k_iter_a, k_iter_b [, all-reduce,
-// k_step_fused]; with caller-side exchange, phase 1 = k_step_fused.  The x / Ax
-// update of each iteration is applied by the next one (bpgl_fused.h).
-int enqueue_phase_fused(bpgl_ctx* c, int64_t it, int phase) {
-    int rc;
-    if (phase == 0) {
-        ev_record(c, it, 0, 0);
-        if ((rc = iter_kernel(c, 0))) return rc;
-        ev_record(c, it, 0, 1);
-        ev_record(c, it, 2, 0);
-        if ((rc = iter_kernel(c, 1))) return rc;
-        ev_record(c, it, 2, 1);
-        if (c->comm) {
-            ev_record(c, it, 4, 0);
-            ncclResult_t nr = ncclAllReduce(c->p.comm, c->p.comm, (size_t)(c->m + 2 + c->nranks), ncclFloat64,
-                                            ncclSum, c->comm, c->stream);
-            if (nr != ncclSuccess) return fail(BPGL_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(nr));
-            ev_record(c, it, 4, 1);
-            ev_record(c, it, 5, 0);
-            hipLaunchKernelGGL(k_step_fused, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
-            LAUNCH_CHECK("k_step_fused");
-            ev_record(c, it, 5, 1);
-        }
-    } else if (c->external) {
-        hipLaunchKernelGGL(k_step_fused, dim3(1), dim3(kStepThreads), 0, c->stream, c->p);
-        LAUNCH_CHECK("k_step_fused");
-    }
-    return 0;
-}
-
-// apply the deferred update of the last fused iteration (no-op when none is pending)
-int finalize_fused(bpgl_ctx* c) {
-    if (!c->fused || !c->solver) return 0;
-    const int64_t n = std::max<int64_t>(c->wp, c->m);
-    const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(n, kThreads), 1024);
-    hipLaunchKernelGGL(k_finalize, dim3(blocks), dim3(kThreads), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_finalize");
-    hipLaunchKernelGGL(k_clear_pending, dim3(1), dim3(64), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_clear_pending");
-    return 0;
-}
-
 // phase 0: colpass, shrink, rowpass, rowreduce [, allreduce, step]; phase 1: update.
 // With the caller doing the exchange (external ranks) phase 0 stops after
 // rowreduce and phase 1 starts with the step.
@@ -571,13 +462,11 @@ int enqueue_phase_onepass_rows(bpgl_ctx* c, int64_t it, int phase) {
         if ((rc = onepass_launch(c))) return rc;
         ev_record(c, it, 7, 1);
         float* xf = xch_f32(c) ? reinterpret_cast<float*>(c->p.comm) : nullptr;
-        if (!c->op.fold) {   // in-kernel fold: k_onepass wrote the exchange buffer itself
-            ev_record(c, it, 3, 0);
-            hipLaunchKernelGGL(k_onepass_fold, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024) + 1),
-                               dim3(kThreads), 0, c->stream, op_params(c), c->op, c->p.comm, xf);
-            LAUNCH_CHECK("k_onepass_fold");
-            ev_record(c, it, 3, 1);
-        }
+        ev_record(c, it, 3, 0);
+        hipLaunchKernelGGL(k_onepass_fold, dim3((unsigned)std::min<int64_t>(cdiv(c->wp, kThreads), 1024) + 1),
+                           dim3(kThreads), 0, c->stream, op_params(c), c->op, c->p.comm, xf);
+        LAUNCH_CHECK("k_onepass_fold");
+        ev_record(c, it, 3, 1);
         if (c->comm) {
             ev_record(c, it, 4, 0);
             if (xf) {
@@ -655,7 +544,6 @@ int enqueue_phase(bpgl_ctx* c, int64_t it, int phase) {
     int rc;
     if (c->op_on) return enqueue_phase_onepass(c, it, phase);
     if (c->rows) return enqueue_phase_rows_twopass(c, it, phase);
-    if (c->fused) return enqueue_phase_fused(c, it, phase);
     const bool multi = c->comm != nullptr || c->external;
     if (phase == 0) {
         ev_record(c, it, 0, 0);
@@ -764,7 +652,7 @@ int step_impl(bpgl_ctx* c, int64_t n_iter) {
         i += k;
         c->op_t += k;
     }
-    return finalize_fused(c);
+    return 0;
 }
 
 // A one-pass launch whose row hand-off ran out of polls (its blocks were not all resident:
@@ -795,7 +683,6 @@ int recover_onepass(bpgl_ctx* c, DevState& st) {
             return fail(BPGL_E_EXCHANGE, "hand-off failure flag set outside the one-pass iteration at t = %lld",
                         (long long)t);
         c->op_on = false;
-        op_configure(c);
         c->n_fallback++;
         if ((rc = capture_graphs(c))) return rc;
         if (!st.done && c->req_t > t && (rc = step_impl(c, c->req_t - t))) return rc;
@@ -809,7 +696,7 @@ int recover_onepass(bpgl_ctx* c, DevState& st) {
 extern "C" {
 
 const char* bpgl_last_error(void) { return bpgl_host::g_err.c_str(); }
-int bpgl_version(void) { return 200; }
+int bpgl_version(void) { return 300; }
 
 int bpgl_stream_create(int device, const uint32_t* cu_mask, int32_t mask_words, void** out) {
     if (!out) return fail(BPGL_E_ARG, "out is null");
@@ -950,9 +837,6 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     p.D = (double*)(s + L.D);
     p.parts = (double*)(s + L.parts);
     p.parts2 = (double*)(s + L.parts2);
-    p.Dbuf = (double*)(s + L.Dbuf);
-    p.cnt_seg = (unsigned long long*)(s + L.cnt);
-    p.cnt_chunk = p.cnt_seg + c->nseg;
     p.reverse_rows = c->reverse_rows;
     p.tail_permille = c->tail_permille;
     p.comm = (double*)(s + L.comm);
@@ -977,19 +861,14 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
         c->op.ls = c->rows ? 0 : 1;   // row shards: the line search follows the all-reduce (in the tail)
         c->op.abe = c->rows ? (double*)(s + L.opABE) : nullptr;
         c->op.cache_permille = op_cache_eff(c);
-        c->op.segcnt = (unsigned long long*)(s + L.opSeg);
-        c->op.Ufold = c->rows ? p.comm : (double*)(s + L.opUsum);
     }
     c->op.fail_at = c->op_fail_at;
     HIP_TRY(hipSetDevice(c->device));
     if (c->op_shape) {
         HIP_TRY(hipMemsetAsync(s + L.opPG, 0, 8 * c->m * c->op_SB, c->stream));   // tag 0: never written
-        HIP_TRY(hipMemsetAsync(s + L.opSeg, 0, 8 * (int64_t)c->op_SB, c->stream));
     }
     HIP_TRY(hipMemsetAsync(s + L.st, 0, sizeof(DevState), c->stream));
     HIP_TRY(hipMemsetAsync(s + L.D, 0, 8 * c->wp, c->stream));
-    HIP_TRY(hipMemsetAsync(s + L.Dbuf, 0, 16 * c->wp, c->stream));
-    HIP_TRY(hipMemsetAsync(s + L.cnt, 0, 8 * ((int64_t)c->nseg + c->nchunk), c->stream));
     if (8ll * c->nchunk * c->wp >= (1ll << 31) || 8ll * c->nseg * c->m >= (1ll << 31))
         return fail(BPGL_E_ARG, "split-K slabs exceed 2 GiB (raise BPGL_TARGET_BLOCKS granularity)");
     c->bound = true;
@@ -1142,9 +1021,7 @@ int bpgl_solver_phase(bpgl_ctx* c, int phase) {
         c->op_refresh_pending = false;
         return onepass_tail<false>(c);
     }
-    if ((rc = enqueue_phase(c, 0, phase))) return rc;
-    if (phase == 1) return finalize_fused(c);
-    return 0;
+    return enqueue_phase(c, 0, phase);
 }
 
 double* bpgl_solver_exchange_buffer(bpgl_ctx* c, int64_t* count) {
@@ -1195,7 +1072,6 @@ int bpgl_solver_reset(bpgl_ctx* c, const double* b, double mu, double* x, const 
         if (c->rows && why && (c->external || !c->op_shape))
             return fail(BPGL_E_ARG, "external row shards run the one-pass iteration only: %s", why);
         c->op_on = c->onepass != 0 && !why;
-        op_configure(c);
         c->op_t = 0;
         c->op_refresh_pending = false;
         // external row shards: the caller runs the first exact gradient (phases 2 and 3)
@@ -1292,29 +1168,9 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         c->solver = false;
         return 0;
     }
-    if (!strcmp(key, "fused")) {
-        c->fused = value != 0;
-        drop_graphs(c);
-        c->solver = false;
-        return 0;
-    }
     if (!strcmp(key, "onepass")) {
         if (value < -1 || value > 1) return fail(BPGL_E_ARG, "onepass must be -1, 0 or 1");
         c->onepass = (int)value;
-        drop_graphs(c);
-        c->solver = false;
-        return 0;
-    }
-    if (!strcmp(key, "onepass_variant")) {
-        if (value < 0 || value >= kOpVariants) return fail(BPGL_E_ARG, "onepass_variant must be in [0, %d)", kOpVariants);
-        c->op_variant = (int)value;
-        drop_graphs(c);
-        c->solver = false;
-        return 0;
-    }
-    if (!strcmp(key, "onepass_fold")) {   // speed only: where the U partials are summed (bitwise neutral for rows)
-        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "onepass_fold must be 0 or 1");
-        c->op_fold = (int)value;
         drop_graphs(c);
         c->solver = false;
         return 0;

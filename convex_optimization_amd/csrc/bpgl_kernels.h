@@ -39,8 +39,6 @@ struct DevState {
     double r1, r2;        // line-search numerators (diagnostics)
     long long iters;      // iterations completed (update applied or stop reached)
     unsigned long long op_ran;   // one-pass mode: k_onepass ran in this iteration (advances op_epoch)
-    long long pending;    // fused mode: the update of iteration t-1 is not yet applied to x / Ax
-    unsigned long long cnt_all;         // fused mode: arrivals of row-chunk finishers in k_iter_b
     long long op_epoch;   // one-pass mode: launches so far (tag of the row-partial hand-off)
     long long op_fail;    // one-pass mode: a hand-off poll ran out (blocks not co-resident)
     unsigned long long op_cnt;   // one-pass mode: row-group arrivals (k_onepass line search)
@@ -76,10 +74,6 @@ struct Params {
     DevState* st;
     double mu, err_bound;
     double wall_tick_s;   // seconds per wall_clock64() tick
-    // fused two-launch iteration (k_iter_a / k_iter_b)
-    double* Dbuf;                    // [2][wp]  direction of iterations with parity 0 / 1
-    unsigned long long* cnt_seg;     // [nseg]   arrivals per column segment (k_iter_a)
-    unsigned long long* cnt_chunk;   // [nchunk] arrivals per row chunk (k_iter_b)
 };
 
 // ---------------------------------------------------------------------------
@@ -514,9 +508,7 @@ __device__ void finish_step(const Params& p, double rs, double ss, double l1bx, 
     st->t = t + 1;
 }
 
-// write-through (sc1) accesses.  8-byte scalars: agent-scope relaxed atomics;
-// split-K slabs: buffer loads / stores with the sc1 cache-policy bit (aux 16),
-// which the compiler batches like ordinary loads.
+// write-through (sc1) accesses of 8-byte scalars: agent-scope relaxed atomics.
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -525,36 +517,6 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
     return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-constexpr int kSC1 = 16;
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double* base, long long bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ void bst2_sc1(__amdgpu_buffer_rsrc_t r, long long off, double a, double b) {
-    const double v[2] = {a, b};
-    u32x4 u;
-    __builtin_memcpy(&u, v, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)off, 0, kSC1);
-}
-__device__ __forceinline__ void bst1_sc1(__amdgpu_buffer_rsrc_t r, long long off, double a) {
-    u32x2 u;
-    __builtin_memcpy(&u, &a, 8);
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)off, 0, kSC1);
-}
-__device__ __forceinline__ void bld2_sc1(__amdgpu_buffer_rsrc_t r, long long off, double& a, double& b) {
-    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSC1);
-    double v[2];
-    __builtin_memcpy(v, &u, 16);
-    a = v[0];
-    b = v[1];
-}
-__device__ __forceinline__ double bld1_sc1(__amdgpu_buffer_rsrc_t r, long long off) {
-    const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kSC1);
-    double v;
-    __builtin_memcpy(&v, &u, 8);
-    return v;
-}
-
 // fold the shrink partials (fixed order) : sum |Bx|, sum |x|, max err
 __device__ void fold_parts(const Params& p, int count, double& a, double& b, double& e) {
     __shared__ double sred[3][kWaves];
@@ -756,7 +718,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(Params p) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         DevState* st = p.st;
-        st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0; st->pending = 0;
+        st->t = 0; st->done = 0; st->block_cnt = 0; st->t_last = -1; st->cur_mb = 0;
         st->gamma = 0.0; st->err = 0.0; st->r1 = 0.0; st->r2 = 0.0; st->iters = 0; st->op_fail = 0;
         st->op_cnt = 0;
         st->op_base = st->op_epoch;

@@ -73,13 +73,6 @@ struct OnePassArgs {
                                  // the residual update (0: the column blocks run it first, as before)
     int tailw;                   // k_onepass_tail, one rank: every lane sums its column's U partials itself
                                  // (wave-owned 64-column tiles, no LDS fold; ngroups <= kOpTailWaveGroups)
-    // in-kernel fold of the U partials ("onepass_fold" = 1): the ngroups blocks of a column segment
-    // meet at segcnt[sb] and each sums one slice of the segment's columns over the row groups
-    int fold;                    // 1: fold inside k_onepass (no k_onepass_fold launch)
-    unsigned long long* segcnt;  // [SB] arrivals per column segment (monotone, + ngroups per launch)
-    double* Ufold;               // [wp] the folded U (one rank: read by the tail; rows: the exchange buffer)
-    float* Ufold32;              // rows, fp32 exchange: the folded U as fp32 (instead of Ufold)
-    int rows_out;                // rows: the last block to arrive writes [r.s23 | s23.s23 | failed] and abe
 };
 
 typedef unsigned long long op_u64;
@@ -151,6 +144,13 @@ __device__ __forceinline__ bool op_failed(const Params& p) {
     return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&p.st->op_fail), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
+// The hand-off needs no agent fences: the partials the last arrival reads (parts2) are stored sc1
+// (st_sc1) by one lane, every wave of the block waits vmcnt(0) before the barrier behind which one
+// lane adds, and the last arrival reads them with sc1 loads (ld_sc1) after its add has returned --
+// row 1 of MI355X_MICROARCH.md's table of hand-offs measured valid with sc1 loads in place of the
+// acquire.  An agent release / acquire pair here writes back the XCD L2 in every block
+// (buffer_wbl2 sc1): measured +3 us per k_onepass launch and +36 us per k_panel_reduce (round 5,
+// profiles/r05/fences), so it is not used.
 __device__ __forceinline__ bool op_arrive_last(unsigned long long* cnt, unsigned long long expected) {
     __shared__ int last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -182,90 +182,12 @@ __device__ void op_linesearch(const Params& p, int ngroups) {
     if (threadIdx.x == 0 && !op_failed(p)) finish_step(p, rs, ss, a, b, e);
 }
 
-// Row shards, in-kernel fold: the last block of the launch to arrive writes the exchange tail
-// [r.s23 | s23.s23 | failed] (fixed-order sums over the row groups, as k_onepass_fold) and the
-// last shrink's folded partials (abe) for the line search at the head of k_onepass_tail.
+// an fp64 scalar as an fp32 hi + lo pair (the fp32 exchange of row shards, k_onepass_fold)
 __device__ __forceinline__ void op_split_f32(double v, float* dst) {
     const float hi = (float)v;
     dst[0] = hi;
     dst[1] = (float)(v - (double)hi);
 }
-__device__ void op_rows_scalars(const Params& p, const OnePassArgs& o) {
-    double a, b, e;
-    fold_parts(p, p.nparts, a, b, e);
-    if (threadIdx.x == 0) {
-        double rs = 0.0, ss = 0.0;
-        for (int q = 0; q < o.ngroups; ++q) { rs += ld_sc1(p.parts2 + 2ll * q); ss += ld_sc1(p.parts2 + 2ll * q + 1); }
-        const bool failed = op_failed(p);
-        if (o.Ufold32) {
-            op_split_f32(rs, o.Ufold32 + p.wp);
-            op_split_f32(ss, o.Ufold32 + p.wp + 2);
-            o.Ufold32[p.wp + 4] = failed ? 1.0f : 0.0f;
-        } else {
-            o.Ufold[p.wp] = rs;
-            o.Ufold[p.wp + 1] = ss;
-            o.Ufold[p.wp + 2] = failed ? 1.0 : 0.0;
-        }
-        o.abe[0] = a;
-        o.abe[1] = b;
-        o.abe[2] = e;
-    }
-}
-
-// In-kernel fold of the U partials (o.fold): every block has written its row group's partial of
-// its column segment through to memory (sc1); the ngroups blocks of segment sb meet at
-// segcnt[sb] (monotone: + ngroups per launch, so the launch's target is the next multiple of
-// ngroups), then block grp sums slice grp of the segment's BC columns over the groups in the
-// fixed order q = 0, 1, ... (the order of k_onepass_fold: the same bits) into Ufold / Ufold32.
-// The wait is bounded like the row hand-off: on exhaustion the launch reports a failure (its
-// blocks were not all resident) and commits nothing.  Returns false on that failure.
-template <int BC>
-__device__ bool op_fold_segment(const Params& p, const OnePassArgs& o, int grp, int sb) {
-    __shared__ int seg_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's partial is in memory
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long* c = o.segcnt + sb;
-        const unsigned long long ng = (unsigned long long)o.ngroups;
-        // release / acquire at agent scope around the meeting: the partials are written and read
-        // through sc1 (write-through / L2-bypassing) already, the fences make the ordering explicit
-        // across XCDs instead of resting on that cache policy
-        __atomic_thread_fence(__ATOMIC_RELEASE);   // agent scope: the HIP default for device code
-        const unsigned long long old = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long target = (old / ng + 1) * ng;
-        unsigned n = kOpPolls;
-        int ok = 1;
-        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (n-- == 0) { ok = 0; break; }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);
-        seg_ok = ok;
-    }
-    __syncthreads();
-    if (!seg_ok) return false;   // block-uniform
-    const int per = (BC + o.ngroups - 1) / o.ngroups;
-    const long long cend = (long long)sb * BC + BC < p.wp ? (long long)sb * BC + BC : p.wp;
-    const __amdgpu_buffer_rsrc_t ru = rsrc(o.Us, 8ll * o.ngroups * p.wp);
-    for (int j = threadIdx.x; j < per; j += kThreads) {
-        const long long c = (long long)sb * BC + (long long)grp * per + j;
-        if (c >= cend) break;
-        double acc = 0.0;
-        int q = 0;
-        for (; q + 8 <= o.ngroups; q += 8) {   // 8 loads in flight, then the adds in group order
-            double v[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = bld1_sc1(ru, 8ll * ((long long)(q + k) * p.wp + c));
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc += v[k];
-        }
-        for (; q < o.ngroups; ++q) acc += bld1_sc1(ru, 8ll * ((long long)q * p.wp + c));
-        if (o.Ufold32) o.Ufold32[c] = (float)acc;
-        else o.Ufold[c] = acc;
-    }
-    return true;
-}
-
 template <int LU, typename T>
 struct OnePassGeo {
     static constexpr int N = VecT<T>::N;
@@ -300,17 +222,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
     if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
         if (sb == 0 && threadIdx.x == 0) { st_sc1(p.parts2 + 2ll * grp, 0.0); st_sc1(p.parts2 + 2ll * grp + 1, 0.0); }
-        if (o.fold) {
-            const __amdgpu_buffer_rsrc_t ru = rsrc(o.Us + (long long)grp * p.wp, 8ll * p.wp);
-            for (int j = threadIdx.x; j < G::BC; j += kThreads)
-                if ((long long)sb * G::BC + j < p.wp) bst1_sc1(ru, 8ll * ((long long)sb * G::BC + j), 0.0);
-            if (!op_fold_segment<G::BC>(p, o, grp, sb) && threadIdx.x == 0)
-                atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
-        }
-        if ((o.ls || o.rows_out) && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) {
-            if (o.ls) op_linesearch(p, o.ngroups);
-            else op_rows_scalars(p, o);
-        }
+        if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) op_linesearch(p, o.ngroups);
         return;
     }
     const unsigned tag = (unsigned)((p.st->op_epoch + 1) & 1);   // bound scratch is zero: parity 0 = unwritten
@@ -495,27 +407,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         if (lane == 0) { st_sc1(p.parts2 + 2ll * grp, rs); st_sc1(p.parts2 + 2ll * grp + 1, ss); }
     }
     double* dst = o.Us + (long long)grp * p.wp;
-    if (o.fold) {   // block-uniform
-        // written through (sc1): the blocks of this segment in the other row groups (other XCDs) read it
-        const __amdgpu_buffer_rsrc_t ru = rsrc(dst, 8ll * p.wp);
 #pragma unroll
-        for (int k = 0; k < LU; ++k)
-            if (colok[k])
+    for (int k = 0; k < LU; ++k)
+        if (colok[k])
 #pragma unroll
-                for (int e = 0; e < N; e += 2) bst2_sc1(ru, 8ll * (col[k] + e), u[k][e], u[k][e + 1]);
-        if (!op_fold_segment<G::BC>(p, o, grp, sb) && threadIdx.x == 0)
-            atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
-    } else {
-#pragma unroll
-        for (int k = 0; k < LU; ++k)
-            if (colok[k])
-#pragma unroll
-                for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
-    }
-    if ((o.ls || o.rows_out) && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) {   // block-uniform
-        if (o.ls) op_linesearch(p, o.ngroups);
-        else op_rows_scalars(p, o);
-    }
+            for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
+    if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) op_linesearch(p, o.ngroups);   // block-uniform
 }
 
 // Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23 |
@@ -648,7 +545,7 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
     }
     const int cb0 = (int)gridDim.x - (UPDATE ? o.rowb : 0);   // column blocks
     const int lane0 = threadIdx.x & 63, wave0 = threadIdx.x >> 6;
-    // pre-summed U (row shards, or one rank after the in-kernel fold), or (tailw) few row-group
+    // pre-summed U (row shards), or (tailw) few row-group
     // partials that each lane sums for its own column: each wave owns 64-column tiles
     const bool wtile = o.ngroups == 1 || o.tailw;
     const long long tile0 = (long long)blockIdx.x * kWaves + wave0;
@@ -763,7 +660,7 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
         p.D[j] = Dj;
     };
     if (wtile) {
-        // U already summed (over ranks, or by k_onepass) or summed per lane: every wave takes its own
+        // U already summed (over ranks) or summed per lane: every wave takes its own
         // 64-column tiles; the first tile's operands were loaded at the head
         // (software-pipelined: the next tile's operands are loaded before this tile's shrink stores,
         // which the compiler could not move them past -- D and x are written in place)

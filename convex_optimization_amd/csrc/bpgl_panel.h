@@ -43,12 +43,12 @@ constexpr int kPanelNA = 3;       // A-side stage buffers (two stages in flight)
 constexpr int kPanelNO = 2;       // k-wide-side stage buffers
 constexpr int kPanelAStage = kPanelRows * kPanelK * 2;   // 32 KiB
 
-// NS: bf16 pieces of the k-wide operand (2: hi + lo, ~16-bit mantissa; 1: hi only).
-// WNX: waves along the RHS (0: 2 when NT >= 2, i.e. 8 waves = 2 per SIMD; 4: 16 waves = 4 per
-// SIMD with half the accumulators each -- the "waves" tuning knob)
-template <int NT, int NS = 2, int WNX = 0>
+// NS: bf16 pieces of the k-wide operand (2: hi + lo, ~16-bit mantissa; 1: hi only).  Waves along
+// the RHS: 2 when NT >= 2, i.e. 8 waves = 2 per SIMD (16 waves with half the accumulators each
+// measured 250-275 / 233-255 us per pass against 236-242 / 219-229, round 2; removed in round 5)
+template <int NT, int NS = 2>
 struct PanelGeo {
-    static constexpr int WN = WNX ? WNX : (NT >= 2 ? 2 : 1);   // waves along the RHS
+    static constexpr int WN = NT >= 2 ? 2 : 1;        // waves along the RHS
     static_assert(NT % WN == 0, "N-tiles per wave");
     static constexpr int NTW = NT / WN;               // N-tiles per wave
     static constexpr int NW = 4 * WN;                 // waves per block
@@ -77,7 +77,7 @@ struct PanelParams {
     long long m, w;
     int nblock, k;
     int kchunks;        // pass-2 split of the block's w columns
-    long long ldr, ldd; // leading dimensions of the bf16 operand images (m, w + the "op_pad" knob)
+    long long ldr, ldd; // leading dimensions of the bf16 operand images (m, w)
     __bf16* Rh;         // [k][ldr]
     __bf16* Rl;
     __bf16* Dh;         // [k][ldd]
@@ -99,49 +99,24 @@ struct PanelParams {
     long long rec_len;
     PanelState* st;
     unsigned long long* cnt;   // [k] k_panel_reduce arrivals per RHS (monotone: launch q ends at q * groups)
-    int wt;             // write-through store sites: 1 pass-1 epilogue (x, D'), 2 pass-2 slab, 4 S, 8 R
     // carried gradient (the "carry_g" knob, one feature block): G_t = G_{t-1} + gamma_{t-1} A^T S_{t-1}
     float* Gc;          // [k][w]   the carried gradient (fp32)
     __bf16* Sh;         // [k][ldr] pass 1's operand in a carried iteration: bf16(V), V = gamma S + E (k_panel_update)
     float* Ec;          // [k][m]   V - bf16(V): the rounding error fed into the next carried operand
-    // e4m3 lo products (the "lo8" knob, section "lo8" below)
-    unsigned* amax;     // float bits of max |A| (k_panel_diag)
-    int* rexp;          // [k][m / 256]   frexp exponent of max |R| per 256-row group (update, reset, refresh)
-    int* dexp;          // [w / 256][k]   frexp exponent of max |D| per 256-column tile (pass-1 epilogue)
 };
 
 constexpr int kLspRows = 1024;    // rows per line-search partial
 
 // Diagnostic builds only (tools/panel_diag.sh; never the shipped library): bit 0 drops the
 // A-side LDS-DMA pieces after the prologue, bit 1 the RHS-side ones, bits 2 / 3 half / all of the
-// lo operand pieces (panel_op_piece), bit 4 the lo MFMAs, bit 5 the lo MFMAs at twice the rate, bit 6 all
-// MFMAs as 32x32x16 -- wrong results, used to split a pass's time into MFMA + LDS and each stream's share.
+// lo operand pieces (panel_op_piece) -- wrong results, used to split a pass's time into MFMA + LDS
+// and each stream's share.  (Round 3's bits 4-6, the lo MFMAs dropped, on e4m3 and on 32x32x16,
+// went with the lo8 and mfma32 forms in rounds 4-5.)
 #ifndef BPGL_PANEL_DIAG
 #define BPGL_PANEL_DIAG 0
 #endif
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
-// diagnostic bit 4: the lo MFMAs are not issued (their fragments are still read) -- the share of a
-// pass that the lo product's matrix-core work costs
-constexpr bool kPanelDiagNoLoMfma = (BPGL_PANEL_DIAG & 16) != 0;
-__device__ __forceinline__ void panel_keep(const bf16x8& v) { asm volatile("" ::"v"(v)); }
-// diagnostic bit 5: the lo product's MFMAs replaced by block-scaled e4m3 ones at twice the bf16 rate
-// (v_mfma_scale_f32_32x32x64_f8f6f4, 4 per wave and stage = half the lo matrix cycles) on the raw bits
-// of the fragments, into accumulators of their own -- the time and clock a 2x-rate lo product would
-// run at, before any conversion cost (results wrong)
-constexpr bool kPanelDiagF8Lo = (BPGL_PANEL_DIAG & 32) != 0;
-// diagnostic bit 6: every hi and lo 16x16x32 MFMA group replaced by the same MACs on 32x32x16 bf16
-// MFMAs (half the operand-register reads per MAC) into accumulators of their own (results wrong) --
-// whether the 32 x 32 shape's lower energy per MAC raises the clock a power-limited pass holds
-constexpr bool kPanelDiag32 = (BPGL_PANEL_DIAG & 64) != 0;
-typedef int i32x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ i32x8 panel_pack8(const bf16x8& x, const bf16x8& y) {
-    i32x8 r;
-    __builtin_memcpy(&r, &x, 16);
-    __builtin_memcpy(reinterpret_cast<char*>(&r) + 16, &y, 16);
-    return r;
-}
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -198,10 +173,10 @@ __device__ __forceinline__ int swz512(int r, int c) { return c ^ (2 * ((r & 3) |
 // this wave (a piece = 8 image rows of 128 B).  When the stage has fewer pieces than waves
 // (NS = 1 at k = 16 or 32) the spare waves issue nothing: the stage's counted wait only
 // assumes that a wave's A pieces are its youngest operations, which still holds.
-template <int NT, int NS, int WNX>
+template <int NT, int NS>
 __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__ hi, const __bf16* __restrict__ lo,
                                                long long ld, long long ks, char* obuf, int wave, int lane) {
-    using G = PanelGeo<NT, NS, WNX>;
+    using G = PanelGeo<NT, NS>;
     const int pc = q * G::NW + wave;
     if (pc * 8 >= NS * G::K) return;   // wave-uniform
     const int rr = pc * 8 + (lane >> 3);
@@ -214,20 +189,20 @@ __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__
     glds16o((hl ? lo : hi) + (long long)rhs * ld + ks + 8 * c, obuf + pc * 1024);
 }
 // pass-1 A stage: rows ks..ks+63 of A, columns col0..col0+255 -> [64][512 B] (a piece = 2 rows)
-template <int NT, int WNX>
+template <int NT>
 __device__ __forceinline__ void panel_a1_piece(int q, const __bf16* __restrict__ A, long long lda, long long ks,
                                                long long col0, char* abuf, int wave, int lane) {
-    using G = PanelGeo<NT, 2, WNX>;
+    using G = PanelGeo<NT, 2>;
     const int pc = q * G::NW + wave;
     const int row = pc * 2 + (lane >> 5);
     const int c = swz512(row, lane & 31);
     glds16a(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
 }
 // pass-2 A stage: rows r0..r0+255 of A, columns ks..ks+63 -> [256][128 B] (a piece = 8 rows)
-template <int NT, int WNX>
+template <int NT>
 __device__ __forceinline__ void panel_a2_piece(int q, const __bf16* __restrict__ A, long long lda, long long r0,
                                                long long ks, char* abuf, int wave, int lane) {
-    using G = PanelGeo<NT, 2, WNX>;
+    using G = PanelGeo<NT, 2>;
     const int pc = q * G::NW + wave;
     const int row = pc * 8 + (lane >> 3);
     const int c = swz128(row, lane & 7);
@@ -265,12 +240,12 @@ __device__ __forceinline__ bf16x8 panel_afrag1(const char* abuf, int j0, int h, 
 // `a_row0`/`a_col0`: PASS 1 -> (first A row of K, first column of the tile); PASS 2 -> (first row, first column of K).
 // ILV 0: a stage's LDS-DMA pieces are issued together after the barrier; ILV 1: they
 // are spread over the stage's MFMA groups (one scheduling group each).  NS: operand pieces.
-template <int NT, int PASS, int ILV, int NS, int WNX>
+template <int NT, int PASS, int ILV, int NS>
 __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restrict__ A, long long lda,
                                                long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
                                                const __bf16* __restrict__ bl, long long ldb, long long b_k0,
-                                               int nsteps, f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
-    using G = PanelGeo<NT, NS, WNX>;
+                                               int nsteps, f32x4 (&acc)[4][PanelGeo<NT, 2>::NTW]) {
+    using G = PanelGeo<NT, NS>;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
@@ -281,24 +256,19 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 #pragma unroll
         for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    f32x16 accd[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) accd[i][e] = 0.f;
     // piece i of stage (so, sa): i < LO -> k-wide piece, else A piece i - LO (this order is what
     // the counted wait below assumes: the youngest LA operations are A pieces)
     auto piece = [&](int i, int so, int bo, int sa, int ba) {
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
-            panel_op_piece<NT, NS, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
+            panel_op_piece<NT, NS>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
                                         wave, lane);
         } else if (PASS == 1) {
-            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+            panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
                                     abufs + ba * kPanelAStage, wave, lane);
         } else {
-            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+            panel_a2_piece<NT>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
                                     abufs + ba * kPanelAStage, wave, lane);
         }
     };
@@ -350,24 +320,10 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
                 bf16x8 b_lo;
                 if constexpr (NS == 2) b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
 #pragma unroll
-                for (int mt = 0; mt < 4 && !kPanelDiag32; ++mt) {
+                for (int mt = 0; mt < 4; ++mt) {
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                    if constexpr (NS == 2 && !kPanelDiagNoLoMfma && !kPanelDiagF8Lo)
+                    if constexpr (NS == 2)
                         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_lo, acc[mt][nt], 0, 0, 0);
-                }
-                if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(b_lo);
-                if constexpr (NS == 2 && kPanelDiagF8Lo && nt % 2 == 0) {
-                    constexpr int i = h * 2 + nt / 2;
-                    accd[i] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-                        panel_pack8(af[(i & 1) * 2], af[(i & 1) * 2 + 1]), panel_pack8(b_hi, b_lo), accd[i], 0, 0, 0, 127, 0,
-                        127);
-                }
-                if constexpr (NS == 2 && kPanelDiag32) {
-                    constexpr int t = (nt >> 1) * 2;
-                    accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], b_hi, accd[t], 0, 0, 0);
-                    accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], b_hi, accd[t + 1], 0, 0, 0);
-                    accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], b_lo, accd[t], 0, 0, 0);
-                    accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[3], b_lo, accd[t + 1], 0, 0, 0);
                 }
                 if constexpr (ILV) {
                     if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
@@ -377,9 +333,6 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
         });
         abuf = abuf == 2 ? 0 : abuf + 1;
     }
-    if constexpr (kPanelDiagF8Lo || kPanelDiag32)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[0][0][0] += accd[i][0] * 0.0f;
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
@@ -389,13 +342,13 @@ __device__ __forceinline__ void panel_mainloop(char* smem, const __bf16* __restr
 // reuse is unchanged (a stage's buffers are refilled only after the barrier that follows
 // all of its reads); all LDS-DMA pieces of a stage are issued before its barrier, spread
 // over the first G - 1 groups.
-template <int NT, int PASS, int NS, int WNX>
+template <int NT, int PASS, int NS>
 __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __restrict__ A, long long lda,
                                                     long long a_row0, long long a_col0,
                                                     const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
                                                     long long ldb, long long b_k0, int nsteps,
-                                                    f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
-    using G = PanelGeo<NT, NS, WNX>;
+                                                    f32x4 (&acc)[4][PanelGeo<NT, 2>::NTW]) {
+    using G = PanelGeo<NT, NS>;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
@@ -409,13 +362,13 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
         if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
         if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
         if (i < G::LO) {
-            panel_op_piece<NT, NS, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
+            panel_op_piece<NT, NS>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
                                         wave, lane);
         } else if (PASS == 1) {
-            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
+            panel_a1_piece<NT>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
                                     abufs + ba * kPanelAStage, wave, lane);
         } else {
-            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
+            panel_a2_piece<NT>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
                                     abufs + ba * kPanelAStage, wave, lane);
         }
     };
@@ -435,11 +388,6 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
         if constexpr (NS == 2) blo = panel_bfrag(ob, G::K + rhs, h, lane);
     };
 
-    f32x16 accd[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) accd[i][e] = 0.f;
     // prologue: op(0), A(0), A(1), then stage 0 landed and group 0's fragments read
     for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
     for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
@@ -477,474 +425,23 @@ __device__ __forceinline__ void panel_mainloop_pipe(char* smem, const __bf16* __
                 read_b(obn, 0, 0, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
             }
 #pragma unroll
-            for (int mt = 0; mt < 4 && !kPanelDiag32; ++mt) {
+            for (int mt = 0; mt < 4; ++mt) {
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][0], acc[mt][nt], 0, 0, 0);
-                if constexpr (NS == 2 && !kPanelDiagNoLoMfma && !kPanelDiagF8Lo)
+                if constexpr (NS == 2)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], bfr[cb][1], acc[mt][nt], 0, 0, 0);
             }
-            if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(bfr[cb][1]);
-            if constexpr (NS == 2 && kPanelDiagF8Lo && nt % 2 == 0) {
-                constexpr int i = h * 2 + nt / 2;
-                accd[i] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-                    panel_pack8(af[ca][(i & 1) * 2], af[ca][(i & 1) * 2 + 1]), panel_pack8(bfr[cb][0], bfr[cb][1]),
-                    accd[i], 0, 0, 0, 127, 0, 127);
-            }
-            if constexpr (NS == 2 && kPanelDiag32) {
-                constexpr int t = (nt >> 1) * 2;
-                accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][0], bfr[cb][0], accd[t], 0, 0, 0);
-                accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][2], bfr[cb][0], accd[t + 1], 0, 0, 0);
-                accd[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][1], bfr[cb][1], accd[t], 0, 0, 0);
-                accd[t + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ca][3], bfr[cb][1], accd[t + 1], 0, 0, 0);
-            }
         });
         abuf = abuf_next;
     }
-    if constexpr (kPanelDiagF8Lo || kPanelDiag32)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[0][0][0] += accd[i][0] * 0.0f;
     wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
 }
 
-// Staggered four-phase form (interleave knob 3; k = 128 with 8 waves: 4 N-tiles per wave).
-// MI355X_MICROARCH.md "Two waves per SIMD": waves w and w + 4 share a SIMD, and in the forms
-// above they run in lockstep -- both read fragments, then both issue MFMAs, so the matrix pipe
-// idles through every read segment.  Here a stage is four phases (h, q): phase (h, 0) reads
-// the A fragments of K-half h and the B fragments of N-tiles 0-1, phase (h, 1) those of
-// N-tiles 2-3; then barrier, 16 MFMAs (4 M-tiles x 2 N-tiles x hi/lo), barrier.  Waves 4-7
-// start one barrier late, so on every SIMD one wave's MFMA segment runs beside its partner's
-// read segment (cdna_hip_programming.md T3/T5: counted vmcnt, raw barriers, setprio around the
-// MFMA cluster).  Stage s's LDS-DMA: O(s+1) and half of A(s+2) in phase 1, the rest of A(s+2)
-// in phase 2 (each slot refilled >= 2 phases after its last read by the later wave group);
-// phase 3 waits until only this wave's A(s+2) pieces are outstanding, so the stage-(s+1) data
-// has landed before the barrier that precedes its first read.
-template <int NT, int PASS, int NS>
-__device__ __forceinline__ void panel_mainloop_stag(char* smem, const __bf16* __restrict__ A, long long lda,
-                                                    long long a_row0, long long a_col0,
-                                                    const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
-                                                    long long ldb, long long b_k0, int nsteps,
-                                                    f32x4 (&acc)[4][PanelGeo<NT, 2, 0>::NTW]) {
-    using G = PanelGeo<NT, NS, 0>;
-    static_assert(G::NTW == 4 && G::NW == 8, "the staggered form is built for 8 waves x 4 N-tiles");
-    static_assert(G::LA % 2 == 0, "A pieces split over two phases");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    char* abufs = smem;
-    char* obufs = smem + kPanelNA * kPanelAStage;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto piece = [&](int i, int so, int bo, int sa, int ba) {
-        if ((BPGL_PANEL_DIAG & 1) && i >= G::LO && (so | sa) != 0) return;
-        if ((BPGL_PANEL_DIAG & 2) && i < G::LO && (so | sa) != 0) return;
-        if (i < G::LO) {
-            panel_op_piece<NT, NS, 0>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage,
-                                      wave, lane);
-        } else if (PASS == 1) {
-            panel_a1_piece<NT, 0>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
-                                  abufs + ba * kPanelAStage, wave, lane);
-        } else {
-            panel_a2_piece<NT, 0>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
-                                  abufs + ba * kPanelAStage, wave, lane);
-        }
-    };
-    constexpr int NP = G::LO + G::LA;
-    // prologue: O(0), A(0), A(1); stage 0 landed; then the stagger
-#pragma unroll
-    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
-#pragma unroll
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
-#pragma unroll
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
-    wait_vm_barrier<G::LA>();
-    if (wn == 1) __builtin_amdgcn_s_barrier();   // waves 4-7: one barrier behind (wave-uniform)
-    bf16x8 af[4];
-    int abuf = 0;
-    for (int s = 0; s < nsteps; ++s) {
-        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
-        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
-        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
-        const char* ab = abufs + abuf * kPanelAStage;
-        const char* ob = obufs + (s & 1) * G::OStage;
-        static_for<0, 4>([&](auto pc) {
-            constexpr int p = decltype(pc)::value;
-            constexpr int h = p >> 1, q = p & 1;
-            if constexpr (q == 0) {
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt)
-                    af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
-                                       : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
-            }
-            bf16x8 bhi[2], blo[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int rhs = (wn * G::NTW + 2 * q + j) * 16 + (lane & 15);
-                bhi[j] = panel_bfrag(ob, rhs, h, lane);
-                if constexpr (NS == 2) blo[j] = panel_bfrag(ob, G::K + rhs, h, lane);
-            }
-            if constexpr (p == 1) {
-                static_for<0, G::LO + G::LA / 2>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
-            } else if constexpr (p == 2) {
-                static_for<G::LO + G::LA / 2, NP>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
-            } else if constexpr (p == 3) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LA) : "memory");
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    acc[mt][2 * q + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bhi[j], acc[mt][2 * q + j], 0, 0, 0);
-                    if constexpr (NS == 2 && !kPanelDiagNoLoMfma)
-                        acc[mt][2 * q + j] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], blo[j], acc[mt][2 * q + j], 0, 0, 0);
-                    if constexpr (NS == 2 && kPanelDiagNoLoMfma) panel_keep(blo[j]);
-                }
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-        });
-        abuf = abuf == 2 ? 0 : abuf + 1;
-    }
-    if (wn == 0) __builtin_amdgcn_s_barrier();   // waves 0-3 take the barrier waves 4-7 took first
-    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
-}
-
-// ---------------------------------------------------------------------------
-// lo8: the lo product on block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, twice the bf16
-// rate).  A k = 128 pass is power-limited: the same ~470k cycles with or without the lo MFMAs, but
-// the bf16 lo product's matrix-core energy pulls the clock from ~2.4 to ~1.9 GHz.
-// Here acc += A (hi) in bf16 as before and acc += A8 (lo8) once per 128 K, where
-//   A8  = e4m3(A / 2^sa): one scale for all of A, max |A| < 2^(sa + 8) (k_panel_diag's max);
-//   lo8 = e4m3(lo / 2^s): per lane (its RHS), |lo| <= 2^(e - 9) for max |v| < 2^e, s = e - 17,
-// so both images stay within +-256 (e4m3fn: +-448); the MFMA's E8M0 scales (127 + sa, 127 + s)
-// undo the division exactly.  The images come from the same bf16 fragments the hi MFMAs read:
-// v_mfma_scale_f32_16x16x128_f8f6f4 pairs byte i of lane l's A operand (row l & 15, K-group l >> 4)
-// with byte i of lane l's B operand (column l & 15, K-group l >> 4) and writes C in the common
-// 16 x 16 layout (tools/mfma_f8_probe.hip, profiles/r03/mfma_f8_probe), so the four 8-value
-// fragments a lane holds for K-half h of stages 2t and 2t + 1 -- byte 8 (2 par + h) + i = element i
-// of the fragment, the same K on both sides -- form one operand, with no lane movement.  Operand
-// precision: e4m3 keeps 4 significant bits, so the lo term carries ~2^-4 of its 2^-9: ~2^-13
-// relative to the product (hi + lo bf16: ~2^-17; d_split = 1: 2^-9).
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-// 8 bf16 -> 8 e4m3 bytes of v / scale (round to nearest even) into dwords 2 SLOT (values 0-3) and
-// 2 SLOT + 1 (values 4-7) of an MFMA operand
-template <int SLOT>
-__device__ __forceinline__ void panel_fp8x8(const bf16x8& v, float scale, i32x8& dst) {
-    s16x2 a = {0, 0}, b = {0, 0};
-    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(a, bf16x2{v[0], v[1]}, scale, false);
-    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(a, bf16x2{v[2], v[3]}, scale, true);
-    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(b, bf16x2{v[4], v[5]}, scale, false);
-    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(b, bf16x2{v[6], v[7]}, scale, true);
-    dst[2 * SLOT] = __builtin_bit_cast(int, a);
-    dst[2 * SLOT + 1] = __builtin_bit_cast(int, b);
-}
-constexpr int kExpZero = -1000;   // exponent recorded for an all-zero group
-__device__ __forceinline__ int panel_frexp(double v) {
-    int e = kExpZero;
-    if (v > 0.0) (void)frexp(v, &e);
-    return e;
-}
-__device__ __forceinline__ int panel_clamp_exp(int s) { return s < -126 ? -126 : (s > 126 ? 126 : s); }
-// scale exponent of a lo piece whose hi + lo values stay below 2^e: |lo| / 2^(e - 17) <= 256
-__device__ __forceinline__ int panel_lo_exp(int e) { return panel_clamp_exp(e - 17); }
-// scale exponent of A's e4m3 image from the max |A| recorded by k_panel_diag: |A| / 2^sa < 256
-__device__ __forceinline__ int panel_a_exp(const unsigned* amax) {
-    int e = 0;
-    (void)frexpf(__uint_as_float(*amax), &e);
-    return panel_clamp_exp(e - 8);
-}
-
-// lane scales of the lo piece: lane l reduces the exponents of RHS wn * RW + l % RW (RW = the wave's
-// RHS), then N-tile nt takes lane nt * 16 + (l & 15)'s result.  All loads are issued before the
-// reduction.  esrc: the pass's exponent table, RHS r over ent entries at esrc[r * erstride + t * etstride].
-template <int NTW>
-__device__ __forceinline__ void panel_lane_scales(const int* __restrict__ esrc, long long erstride, long long etstride,
-                                                  int ent, int wn, int lane, float (&b_sc)[NTW], int (&b_e8)[NTW]) {
-    constexpr int RW = NTW * 16;
-    int emax = kExpZero;
-    const int* er = esrc + (long long)(wn * RW + lane % RW) * erstride;
-    for (int t0 = 0; t0 < ent; t0 += 32) {
-        int ev[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) ev[t] = t0 + t < ent ? er[(long long)(t0 + t) * etstride] : kExpZero;
-#pragma unroll
-        for (int t = 0; t < 32; ++t) emax = ev[t] > emax ? ev[t] : emax;
-    }
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-        const int sb = panel_lo_exp(__shfl(emax, nt * 16 + (lane & 15)));
-        b_sc[nt] = ldexpf(1.0f, sb);
-        b_e8[nt] = 127 + sb;
-    }
-}
-
-// The ILV 0 / 1 mainloop (panel_mainloop) with the lo product on e4m3, stages taken in pairs
-// (nsteps must be even: the host requires 128 | the pass's K range).  esrc: this pass's exponent
-// table, lane RHS r over ent entries at esrc[r * erstride + t * etstride]; the lane scale is the
-// max over them.  a_exp: A's scale exponent.
-template <int NT, int PASS, int ILV, int WNX>
-__device__ __forceinline__ void panel_mainloop_lo8(char* smem, const __bf16* __restrict__ A, long long lda,
-                                                   long long a_row0, long long a_col0, const __bf16* __restrict__ bh,
-                                                   const __bf16* __restrict__ bl, long long ldb, long long b_k0,
-                                                   int nsteps, const int* __restrict__ esrc, long long erstride,
-                                                   long long etstride, int ent, int a_exp,
-                                                   f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
-    using G = PanelGeo<NT, 2, WNX>;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    char* abufs = smem;
-    char* obufs = smem + kPanelNA * kPanelAStage;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float b_sc[G::NTW];
-    int b_e8[G::NTW];
-    panel_lane_scales<G::NTW>(esrc, erstride, etstride, ent, wn, lane, b_sc, b_e8);
-    const float a_sc = ldexpf(1.0f, a_exp);
-    const int a_e8 = 127 + a_exp;
-
-    auto piece = [&](int i, int so, int bo, int sa, int ba) {
-        if (i < G::LO) {
-            panel_op_piece<NT, 2, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
-                                       lane);
-        } else if (PASS == 1) {
-            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
-                                    abufs + ba * kPanelAStage, wave, lane);
-        } else {
-            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
-                                    abufs + ba * kPanelAStage, wave, lane);
-        }
-    };
-    constexpr int NP = G::LO + G::LA;
-    constexpr int NG = 2 * G::NTW;
-    constexpr int PPG = (NP + NG - 1) / NG;
-    // prologue: op(0), A(0), A(1) -- the loop's counted wait assumes exactly this issue order
-#pragma unroll
-    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
-#pragma unroll
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
-#pragma unroll
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
-    i32x8 a8[4], b8[G::NTW];
-    int abuf = 0;
-    auto stage = [&](int s, auto parc) {
-        constexpr int par = decltype(parc)::value;
-        wait_vm_barrier<G::LA>();
-        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
-        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
-        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
-        if (!ILV) {
-#pragma unroll
-            for (int i = 0; i < NP; ++i) piece(i, so, bo, sa, ba);
-        }
-        const char* ab = abufs + abuf * kPanelAStage;
-        const char* ob = obufs + (s & 1) * G::OStage;
-        static_for<0, 2>([&](auto hc) {
-            constexpr int h = decltype(hc)::value;
-            constexpr int slot = 2 * par + h;
-            bf16x8 af[4];
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-                af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
-                                   : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) panel_fp8x8<slot>(af[mt], a_sc, a8[mt]);
-            static_for<0, G::NTW>([&](auto ntc) {
-                constexpr int nt = decltype(ntc)::value;
-                constexpr int grp = h * G::NTW + nt;
-                constexpr int p0 = grp * PPG < NP ? grp * PPG : NP;
-                constexpr int p1 = (grp + 1) * PPG < NP ? (grp + 1) * PPG : NP;
-                if constexpr (ILV) {
-                    static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
-                }
-                const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
-                const bf16x8 b_hi = panel_bfrag(ob, rhs, h, lane);
-                const bf16x8 b_lo = panel_bfrag(ob, G::K + rhs, h, lane);
-                panel_fp8x8<slot>(b_lo, b_sc[nt], b8[nt]);
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], b_hi, acc[mt][nt], 0, 0, 0);
-                if constexpr (par == 1 && h == 1) {
-#pragma unroll
-                    for (int mt = 0; mt < 4; ++mt)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                            a8[mt], b8[nt], acc[mt][nt], 0, 0, 0, a_e8, 0, b_e8[nt]);
-                }
-                if constexpr (ILV) {
-                    if constexpr (p1 > p0) __builtin_amdgcn_sched_group_barrier(0x20, p1 - p0, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x8, (par == 1 && h == 1) ? 8 : 4, 0);
-                }
-            });
-        });
-        abuf = abuf == 2 ? 0 : abuf + 1;
-    };
-    for (int s = 0; s < nsteps; s += 2) {
-        stage(s, std::integral_constant<int, 0>{});
-        stage(s + 1, std::integral_constant<int, 1>{});
-    }
-    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
-}
-
-// The software-pipelined mainloop (panel_mainloop_pipe, interleave 2: fragments read one MFMA group
-// ahead, the stage barrier before a stage's last group) with the lo product on e4m3, stages in pairs.
-// A's fragments of K-half h are converted at the group that first uses them (nt = 0), a lo fragment
-// at its own group; the e4m3 MFMAs of N-tile nt follow its hi MFMAs in the group (odd stage, h = 1).
-template <int NT, int PASS, int WNX>
-__device__ __forceinline__ void panel_mainloop_pipe_lo8(char* smem, const __bf16* __restrict__ A, long long lda,
-                                                        long long a_row0, long long a_col0,
-                                                        const __bf16* __restrict__ bh, const __bf16* __restrict__ bl,
-                                                        long long ldb, long long b_k0, int nsteps,
-                                                        const int* __restrict__ esrc, long long erstride,
-                                                        long long etstride, int ent, int a_exp,
-                                                        f32x4 (&acc)[4][PanelGeo<NT, 2, WNX>::NTW]) {
-    using G = PanelGeo<NT, 2, WNX>;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 3, wn = wave >> 2;
-    char* abufs = smem;
-    char* obufs = smem + kPanelNA * kPanelAStage;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < G::NTW; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float b_sc[G::NTW];
-    int b_e8[G::NTW];
-    panel_lane_scales<G::NTW>(esrc, erstride, etstride, ent, wn, lane, b_sc, b_e8);
-    const float a_sc = ldexpf(1.0f, a_exp);
-    const int a_e8 = 127 + a_exp;
-    auto piece = [&](int i, int so, int bo, int sa, int ba) {
-        if (i < G::LO) {
-            panel_op_piece<NT, 2, WNX>(i, bh, bl, ldb, b_k0 + (long long)so * kPanelK, obufs + bo * G::OStage, wave,
-                                       lane);
-        } else if (PASS == 1) {
-            panel_a1_piece<NT, WNX>(i - G::LO, A, lda, a_row0 + (long long)sa * kPanelK, a_col0,
-                                    abufs + ba * kPanelAStage, wave, lane);
-        } else {
-            panel_a2_piece<NT, WNX>(i - G::LO, A, lda, a_row0, a_col0 + (long long)sa * kPanelK,
-                                    abufs + ba * kPanelAStage, wave, lane);
-        }
-    };
-    constexpr int NP = G::LO + G::LA;
-    constexpr int NG = 2 * G::NTW;
-    constexpr int NGI = NG > 1 ? NG - 1 : 1;
-    constexpr int PPG = (NP + NGI - 1) / NGI;
-    auto read_a = [&](const char* ab, int h, bf16x8 (&af)[4]) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-            af[mt] = PASS == 1 ? panel_afrag1(ab, wm * 64 + mt * 16, h, lane)
-                               : panel_afrag2(ab, wm * 64 + mt * 16 + (lane & 15), h, lane);
-    };
-    auto read_b = [&](const char* ob, int h, int nt, bf16x8& bhi, bf16x8& blo) {
-        const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
-        bhi = panel_bfrag(ob, rhs, h, lane);
-        blo = panel_bfrag(ob, G::K + rhs, h, lane);
-    };
-    for (int i = 0; i < G::LO; ++i) piece(i, 0, 0, 0, 0);
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, 0, 0);
-    for (int i = G::LO; i < NP; ++i) piece(i, 0, 0, nsteps > 1 ? 1 : 0, 1);
-    wait_vm_barrier<G::LA>();
-    bf16x8 af[2][4];
-    bf16x8 bfr[2][2];
-    read_a(abufs, 0, af[0]);
-    read_b(obufs, 0, 0, bfr[0][0], bfr[0][1]);
-    i32x8 a8[4], b8[G::NTW];
-    int abuf = 0;
-    auto stage = [&](int s, auto parc) {
-        constexpr int par = decltype(parc)::value;
-        const int so = s + 1 < nsteps ? s + 1 : nsteps - 1;     // clamped tail: loads into unread buffers
-        const int sa = s + 2 < nsteps ? s + 2 : nsteps - 1;
-        const int bo = (s + 1) & 1, ba = abuf == 0 ? 2 : abuf - 1;   // (s + 2) % 3
-        const int abuf_next = abuf == 2 ? 0 : abuf + 1;
-        const char* ab = abufs + abuf * kPanelAStage;
-        const char* ob = obufs + (s & 1) * G::OStage;
-        static_for<0, NG>([&](auto gc) {
-            constexpr int g = decltype(gc)::value;
-            constexpr int h = g / G::NTW, nt = g % G::NTW;
-            constexpr int cb = g & 1, ca = h & 1;
-            constexpr int slot = 2 * par + h;
-            constexpr int p0 = g < NGI ? (g * PPG < NP ? g * PPG : NP) : NP;
-            constexpr int p1 = g < NGI ? ((g + 1) * PPG < NP ? (g + 1) * PPG : NP) : NP;
-            static_for<p0, p1>([&](auto ic) { piece(decltype(ic)::value, so, bo, sa, ba); });
-            if constexpr (nt == 0) {
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt) panel_fp8x8<slot>(af[ca][mt], a_sc, a8[mt]);
-            }
-            panel_fp8x8<slot>(bfr[cb][1], b_sc[nt], b8[nt]);
-            const bf16x8 b_hi = bfr[cb][0];
-            if constexpr (g + 1 < NG) {
-                constexpr int h1 = (g + 1) / G::NTW, nt1 = (g + 1) % G::NTW;
-                if constexpr (h1 != h) read_a(ab, h1, af[h1 & 1]);
-                read_b(ob, h1, nt1, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
-            } else {
-                wait_vm_barrier<G::LA>();   // stage s + 1 landed (only A(s+2) may be outstanding)
-                const char* abn = abufs + abuf_next * kPanelAStage;
-                const char* obn = obufs + ((s + 1) & 1) * G::OStage;
-                read_a(abn, 0, af[0]);   // the last group runs on af[1] (h = 1)
-                read_b(obn, 0, 0, bfr[cb ^ 1][0], bfr[cb ^ 1][1]);
-            }
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ca][mt], b_hi, acc[mt][nt], 0, 0, 0);
-            if constexpr (par == 1 && h == 1) {
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[mt], b8[nt], acc[mt][nt], 0, 0, 0,
-                                                                                   a_e8, 0, b_e8[nt]);
-            }
-        });
-        abuf = abuf_next;
-    };
-    for (int s = 0; s < nsteps; s += 2) {
-        stage(s, std::integral_constant<int, 0>{});
-        stage(s + 1, std::integral_constant<int, 1>{});
-    }
-    wait_vm_barrier<0>();   // the clamped tail loads have landed; LDS free for the epilogue
-}
-
-// Write-through (sc1) stores for the bulk outputs a kernel hands to the next launch (split-K
-// slab, D', x, S, R and its split): the lines do not sit dirty in the XCD L2s at the kernel
-// boundary, whose cost grows by ~1 us per 6 MB left dirty (MI355X_MICROARCH.md, "boundary").
-// The resource is uniform (a buffer's base); the per-lane part is a byte offset (< 2^31).
-typedef unsigned int pu32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int pu32x2 __attribute__((ext_vector_type(2)));
-constexpr int kPanelSC1 = 16;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
-}
-template <typename V>
-__device__ __forceinline__ void wt_store16(__amdgpu_buffer_rsrc_t r, long long byte_off, const V& v) {
-    static_assert(sizeof(V) == 16, "16-byte store");
-    pu32x4 u;
-    __builtin_memcpy(&u, &v, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)byte_off, 0, kPanelSC1);
-}
-template <typename V>
-__device__ __forceinline__ void wt_store8(__amdgpu_buffer_rsrc_t r, long long byte_off, const V& v) {
-    static_assert(sizeof(V) == 8, "8-byte store");
-    pu32x2 u;
-    __builtin_memcpy(&u, &v, 8);
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)byte_off, 0, kPanelSC1);
-}
-// element e of a buffer of `count` elements: write-through when `on` (PanelParams::wt, the
-// "write_through" knob) and the buffer's bytes fit a buffer offset (wave-uniform tests), a
-// plain store otherwise
+// Plain 16- / 8-byte stores for the outputs a kernel hands to the next launch.  (Round 2's
+// write-through (sc1) variant of these stores -- the "write_through" knob -- measured <= 0.6 % and
+// cost the pass-1 epilogue 18 us; removed in round 5.)
 template <typename V, typename E>
-__device__ __forceinline__ void wt_put(bool on, E* base, long long count, long long e, const V& v) {
-    if (on && count * (long long)sizeof(E) < (1ll << 31)) {
-        if constexpr (sizeof(V) == 16) wt_store16(wt_rsrc(base), e * (long long)sizeof(E), v);
-        else wt_store8(wt_rsrc(base), e * (long long)sizeof(E), v);
-    } else {
-        *reinterpret_cast<V*>(base + e) = v;
-    }
+__device__ __forceinline__ void put(E* base, long long e, const V& v) {
+    *reinterpret_cast<V*>(base + e) = v;
 }
 
 __device__ __forceinline__ void split_bf16(double v, __bf16& hi, __bf16& lo) {
@@ -980,7 +477,7 @@ template <int DS, int GM>
 __device__ __forceinline__ void panel_shrink4(const f32x4& acc, const float (&xs)[4], float (&gs)[4],
                                               const double (&dgv)[4], const double (&rcv)[4], double mu,
                                               __bf16 (&dh)[4], __bf16 (&dl)[4], double& sbx, double& sx,
-                                              double& err, double& dmax) {
+                                              double& err) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         double g = (double)acc[r];
@@ -989,7 +486,6 @@ __device__ __forceinline__ void panel_shrink4(const f32x4& acc, const float (&xs
         const double x = (double)xs[r];
         const double bx = rcv[r] * soft_thr(dgv[r] * x - g, mu);
         double dprime;
-        dmax = fmax(dmax, fabs(bx - x));
         if constexpr (DS == 2) {
             split_bf16(bx - x, dh[r], dl[r]);
             dprime = (double)(float)dh[r] + (double)(float)dl[r];
@@ -1005,45 +501,38 @@ __device__ __forceinline__ void panel_shrink4(const f32x4& acc, const float (&xs
 }
 // the per-RHS partials of one wave's RHS tile (lanes l, l^16, l^32, l^48 share the RHS) -> nred
 __device__ __forceinline__ void panel_norms_wave(double* nred, int wm, int K, int rhs, double sbx, double sx,
-                                                 double err, double dmax) {
+                                                 double err) {
     const int lane = threadIdx.x & 63;
     sbx += __shfl_xor(sbx, 16); sbx += __shfl_xor(sbx, 32);
     sx += __shfl_xor(sx, 16);   sx += __shfl_xor(sx, 32);
     { double o = __shfl_xor(err, 16); err = (o > err || o != o) ? o : err;
       o = __shfl_xor(err, 32); err = (o > err || o != o) ? o : err; }
-    dmax = fmax(dmax, __shfl_xor(dmax, 16)); dmax = fmax(dmax, __shfl_xor(dmax, 32));
     if (lane < 16) {
         double* d = nred + ((long long)wm * K + rhs) * 4;
         d[0] = sbx;
         d[1] = sx;
         d[2] = err;
-        d[3] = dmax;
+        d[3] = 0.0;
     }
 }
 // the block's norms per RHS from the four column groups' partials (after a barrier)
 __device__ __forceinline__ void panel_norms_out(const PanelParams& p, const double* nred, int T) {
     const int K = p.k;
     for (int rhs = threadIdx.x; rhs < K; rhs += T) {
-        double a = 0.0, b = 0.0, e = 0.0, dm = 0.0;
+        double a = 0.0, b = 0.0, e = 0.0;
         for (int q = 0; q < 4; ++q) {
             const double* d = nred + ((long long)q * K + rhs) * 4;
             a += d[0];
             b += d[1];
             e = (d[2] > e || d[2] != d[2]) ? d[2] : e;
-            dm = fmax(dm, d[3]);
         }
         double* dst = p.norms + ((long long)blockIdx.x * p.k + rhs) * 4;
         dst[0] = a; dst[1] = b; dst[2] = e; dst[3] = 0.0;
-        // the tile's max |D| for the e4m3 scale of the direction's lo piece in pass 2 (lo8)
-        if (p.dexp) p.dexp[(long long)blockIdx.x * p.k + rhs] = panel_frexp(dm);
     }
 }
 
 // BPGL_PANEL_DIAG (timing-only builds, tools/panel_epi_diag.sh; results wrong): bit 0 -- no carried-G
 // store, bit 1 -- no D' store, bit 3 -- no epilogue loop at all (the products are only kept alive)
-#ifndef BPGL_PANEL_DIAG
-#define BPGL_PANEL_DIAG 0
-#endif
 template <int NTW, int EPI, int DS, int GM = 0, int NW = 0>
 __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int mb, long long c0, int wm, int wn,
                                                      int T, f32x4 (&acc)[4][NTW], char* smem,
@@ -1136,7 +625,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             const int rhs = (wn * 4 + nt) * 16 + (lane & 15);
             const double mu = reinterpret_cast<const double*>(dgl + 4096)[rhs];
             const double gprev = fx ? reinterpret_cast<const double*>(dgl + 5120)[rhs] : 0.0;
-            double sbx = 0.0, sx = 0.0, err = 0.0, dmax = 0.0;
+            double sbx = 0.0, sx = 0.0, err = 0.0;
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
                 const int cc = wm * 64 + mt * 16 + (lane >> 4) * 4;   // column within the block
@@ -1169,19 +658,19 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                         if constexpr (DS == 2) dq += (double)(float)lq[r];
                         xs[r] = (float)((double)xs[r] + gprev * dq);
                     }
-                    wt_put(p.wt & 1, p.X, (long long)p.nblock * p.k * p.w, ((long long)mb * p.k + rhs) * p.w + j,
+                    put(p.X, ((long long)mb * p.k + rhs) * p.w + j,
                            make_float4(xs[0], xs[1], xs[2], xs[3]));
                 }
                 __bf16 dh[4], dl[4];
-                panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err, dmax);
+                panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err);
                 if constexpr (GM != 0)   // read again only next iteration, after all of A: non-temporal
                     __builtin_nontemporal_store(f32x4{gs[0], gs[1], gs[2], gs[3]},
                                                 reinterpret_cast<f32x4*>(p.Gc + (long long)rhs * p.w + j));
-                wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
+                put(p.Dh, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
                 if constexpr (DS == 2)
-                    wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
+                    put(p.Dl, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
             }
-            panel_norms_wave(nrd, wm, K, rhs, sbx, sx, err, dmax);
+            panel_norms_wave(nrd, wm, K, rhs, sbx, sx, err);
             if (nt + 2 < 4) {
                 __syncthreads();                      // every wave is done with this phase's buffer
                 lddp(nt + 2);
@@ -1234,7 +723,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
         const int rhs = (wn * NTW + nt) * 16 + (lane & 15);
         const double mu = muv[nt];
         const double gprev = gpv[nt];
-        double sbx = 0.0, sx = 0.0, err = 0.0, dmax = 0.0;
+        double sbx = 0.0, sx = 0.0, err = 0.0;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
             const long long j = jl + mt * 16;   // 4 consecutive columns
@@ -1264,7 +753,7 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                     if constexpr (DS == 2) dq += (double)(float)lq[r];
                     xs[r] = (float)((double)xs[r] + gprev * dq);
                 }
-                wt_put(p.wt & 1, p.X, (long long)p.nblock * p.k * p.w, ((long long)mb * p.k + rhs) * p.w + j,
+                put(p.X, ((long long)mb * p.k + rhs) * p.w + j,
                        make_float4(xs[0], xs[1], xs[2], xs[3]));
             }
             __bf16 dh[4], dl[4];
@@ -1277,17 +766,17 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
             float gs[4] = {gq.x, gq.y, gq.z, gq.w};
             const double dgv[4] = {dq01.x, dq01.y, dq23.x, dq23.y};
             const double rcv[4] = {rq01.x, rq01.y, rq23.x, rq23.y};
-            panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err, dmax);
+            panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err);
             if constexpr (GM != 0 && (BPGL_PANEL_DIAG & 1) == 0)
                 *reinterpret_cast<float4*>(p.Gc + (long long)rhs * p.w + j) = make_float4(gs[0], gs[1], gs[2], gs[3]);
             if constexpr ((BPGL_PANEL_DIAG & 2) == 0)
-            wt_put(p.wt & 1, p.Dh, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
+            put(p.Dh, (long long)rhs * p.ldd + j, bf16x4{dh[0], dh[1], dh[2], dh[3]});
             if constexpr (DS == 2)
-                wt_put(p.wt & 1, p.Dl, (long long)p.k * p.ldd, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
+                put(p.Dl, (long long)rhs * p.ldd + j, bf16x4{dl[0], dl[1], dl[2], dl[3]});
             xq = xn; gq = gn; hq1 = hn1;
             dq01 = dn01; dq23 = dn23; rq01 = rn01; rq23 = rn23;
         }
-        panel_norms_wave(nred, wm, K, rhs, sbx, sx, err, dmax);
+        panel_norms_wave(nred, wm, K, rhs, sbx, sx, err);
     }
     __syncthreads();
     panel_norms_out(p, nred, T);
@@ -1298,10 +787,10 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
 // epilogue (EPI 1: the direction D' in DS bf16 pieces (2: Dh + Dl, 1: Dh alone), norms
 // per RHS).  grid = w / 256 blocks.  R always enters as hi + lo.
 // ---------------------------------------------------------------------------
-template <int NT, int EPI, int ILV, int DS, int WNX, int L8 = 0, int GM = 0>
-__global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
+template <int NT, int EPI, int ILV, int DS, int GM = 0>
+__global__ __launch_bounds__((PanelGeo<NT, 2>::T)) void k_panel_pass1(PanelParams p, int fixed_block,
                                                                          double* __restrict__ Gout) {
-    using G = PanelGeo<NT, 2, WNX>;
+    using G = PanelGeo<NT, 2>;
     __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1310,30 +799,20 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
     f32x4 acc[4][G::NTW];
     if constexpr (GM == 2) {   // carried iteration: U = A^T bf16(V_{t-1}), one bf16 operand
         if constexpr (ILV >= 2)
-            panel_mainloop_pipe<NT, 1, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
-                                               (int)(p.m / kPanelK), acc);
+            panel_mainloop_pipe<NT, 1, 1>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
+                                          (int)(p.m / kPanelK), acc);
         else
-            panel_mainloop<NT, 1, ILV, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
-                                               (int)(p.m / kPanelK), acc);
+            panel_mainloop<NT, 1, ILV, 1>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
+                                          (int)(p.m / kPanelK), acc);
         panel_pass1_epilogue<G::NTW, EPI, DS, 2, G::NW>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
         return;
-    } else if constexpr (L8 && ILV >= 2)   // the residual's lo piece on e4m3: scales from the 256-row groups' max |R|
-        panel_mainloop_pipe_lo8<NT, 1, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
-                                            (int)(p.m / kPanelK), p.rexp, p.m / kPanelRows, 1,
-                                            (int)(p.m / kPanelRows), panel_a_exp(p.amax), acc);
-    else if constexpr (L8)
-        panel_mainloop_lo8<NT, 1, ILV, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
-                                            (int)(p.m / kPanelK), p.rexp, p.m / kPanelRows, 1,
-                                            (int)(p.m / kPanelRows), panel_a_exp(p.amax), acc);
-    else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
-        panel_mainloop_stag<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
+    }
+    if constexpr (ILV >= 2)
+        panel_mainloop_pipe<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                       (int)(p.m / kPanelK), acc);
-    else if constexpr (ILV >= 2)
-        panel_mainloop_pipe<NT, 1, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
-                                           (int)(p.m / kPanelK), acc);
     else
-        panel_mainloop<NT, 1, ILV, 2, WNX>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
-                                           (int)(p.m / kPanelK), acc);
+        panel_mainloop<NT, 1, ILV, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
+                                      (int)(p.m / kPanelK), acc);
 
     panel_pass1_epilogue<G::NTW, EPI, DS, GM, G::NW>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
 }
@@ -1342,9 +821,9 @@ __global__ __launch_bounds__((PanelGeo<NT, 2, WNX>::T)) void k_panel_pass1(Panel
 // pass 2: partial S over one column chunk: Sslab[chunk][rhs][row]; the direction in NS
 // bf16 pieces.  grid = (m / 256) x kchunks
 // ---------------------------------------------------------------------------
-template <int NT, int ILV, int NS, int WNX, int L8 = 0>
-__global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(PanelParams p, int fixed_block) {
-    using G = PanelGeo<NT, NS, WNX>;
+template <int NT, int ILV, int NS>
+__global__ __launch_bounds__((PanelGeo<NT, NS>::T)) void k_panel_pass2(PanelParams p, int fixed_block) {
+    using G = PanelGeo<NT, NS>;
     __shared__ __attribute__((aligned(16))) char smem[G::Smem];
     const int mb = fixed_block >= 0 ? fixed_block : (int)(p.st->t % p.nblock);
     const int lane = threadIdx.x & 63;
@@ -1366,33 +845,19 @@ __global__ __launch_bounds__((PanelGeo<NT, NS, WNX>::T)) void k_panel_pass2(Pane
     const long long kc = p.w / p.kchunks;
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
-    if constexpr (L8 && NS == 2 && ILV >= 2)   // the direction's lo piece on e4m3: scales from the chunk's tiles' max |D|
-        panel_mainloop_pipe_lo8<NT, 2, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
-                                            p.ldd, chunk * kc, (int)(kc / kPanelK),
-                                            p.dexp + (chunk * kc / kPanelRows) * p.k, 1, p.k,
-                                            (int)((chunk * kc % kPanelRows + kc + kPanelRows - 1) / kPanelRows),
-                                            panel_a_exp(p.amax), acc);
-    else if constexpr (L8 && NS == 2)
-        panel_mainloop_lo8<NT, 2, ILV, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
-                                            chunk * kc, (int)(kc / kPanelK), p.dexp + (chunk * kc / kPanelRows) * p.k,
-                                            1, p.k, (int)((chunk * kc % kPanelRows + kc + kPanelRows - 1) / kPanelRows),
-                                            panel_a_exp(p.amax), acc);
-    else if constexpr (ILV == 3 && WNX == 0 && G::NTW == 4)
-        panel_mainloop_stag<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
+    if constexpr (ILV >= 2)
+        panel_mainloop_pipe<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);
-    else if constexpr (ILV >= 2)
-        panel_mainloop_pipe<NT, 2, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
-                                            p.ldd, chunk * kc, (int)(kc / kPanelK), acc);
     else
-        panel_mainloop<NT, 2, ILV, NS, WNX>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl,
-                                            p.ldd, chunk * kc, (int)(kc / kPanelK), acc);
+        panel_mainloop<NT, 2, ILV, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
+                                       chunk * kc, (int)(kc / kPanelK), acc);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < G::NTW; ++nt) {
             const int rhs = (wn * G::NTW + nt) * 16 + (lane & 15);
             const long long row = r0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
-            wt_put(p.wt & 2, p.Sslab, (long long)p.kchunks * p.k * p.m, ((long long)chunk * p.k + rhs) * p.m + row,
+            put(p.Sslab, ((long long)chunk * p.k + rhs) * p.m + row,
                    make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]));
         }
 }
@@ -1459,8 +924,8 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
         }
         for (; c < p.kchunks; ++c) add(*reinterpret_cast<const float4*>(src + c * cstride));
         const long long e = (long long)rhs * p.m + i;
-        wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e, make_double2(s[0], s[1]));
-        wt_put(p.wt & 4, Sout, (long long)p.k * p.m, e + 2, make_double2(s[2], s[3]));
+        put(Sout, e, make_double2(s[0], s[1]));
+        put(Sout, e + 2, make_double2(s[2], s[3]));
         if (mode) {
             rs = fma(r01.x, s[0], rs); rs = fma(r01.y, s[1], rs);
             rs = fma(r23.x, s[2], rs); rs = fma(r23.y, s[3], rs);
@@ -1481,6 +946,9 @@ __global__ __launch_bounds__(kThreads) void k_panel_reduce(PanelParams p, double
         panel_st_sc1(dst, ((sr[0] + sr[1]) + sr[2]) + sr[3]);
         panel_st_sc1(dst + 1, ((sq[0] + sq[1]) + sq[2]) + sq[3]);
         const unsigned long long ng = (unsigned long long)((p.m + kLspRows - 1) / kLspRows);
+        // no agent fences: the partials are stored sc1 by this lane, which waits vmcnt(0) before its
+        // add, and the last block reads them sc1 after its add returned (row 1 of MI355X_MICROARCH.md's
+        // table of sc1 hand-offs; the fence pair measured +36 us per launch, see op_arrive_last)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long old = __hip_atomic_fetch_add(p.cnt + rhs, 1ull, __ATOMIC_RELAXED,
                                                               __HIP_MEMORY_SCOPE_AGENT);
@@ -1550,17 +1018,6 @@ __device__ __forceinline__ void panel_bump_t(const PanelParams& p, bool pending)
         p.st->iters = t + 1;
         if (pending) p.st->pending = 1;
     }
-}
-
-// lo8: the max |R| of the 256 residual rows a wave's 64 units (4 rows each, one RHS) hold -> the
-// exponent table pass 1 scales the residual's lo piece by.  v: this lane's unit in [k][m / 4]; the
-// wave's units are v0 .. v0 + 63 with 64 | v0 (the callers' unit ranges are multiples of 64), so
-// the wave's group is v0 / 64 of [k][m / 256].  Whole waves only (wave_max).
-__device__ __forceinline__ void panel_put_rexp(const PanelParams& p, unsigned v, const double (&r)[4]) {
-    if (!p.rexp) return;
-    double mx = fmax(fmax(fabs(r[0]), fabs(r[1])), fmax(fabs(r[2]), fabs(r[3])));
-    mx = wave_max(mx);
-    if ((threadIdx.x & 63) == 0) p.rexp[v / 64] = panel_frexp(mx);
 }
 
 // carried gradient (one feature block): the next pass 1's operand V = gamma S + E (cflag & 3 == 1; 2: the
@@ -1659,13 +1116,12 @@ __global__ __launch_bounds__(kThreads) void k_panel_update(PanelParams p, int cf
                     split_bf16(r[q], hi[q], lo[q]);
                 }
             }
-            wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
-            wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
+            put(p.R, e, make_double2(r[0], r[1]));
+            put(p.R, e + 2, make_double2(r[2], r[3]));
             if (!(cflag & 4)) {
-                wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
-                wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+                put(p.Rh, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+                put(p.Rl, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
             }
-            panel_put_rexp(p, v, r);
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, false);
@@ -1692,13 +1148,12 @@ __global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p, int c
         __bf16 hi[4], lo[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) split_bf16(r[q], hi[q], lo[q]);
-        wt_put(p.wt & 8, p.R, nr, e, make_double2(r[0], r[1]));
-        wt_put(p.wt & 8, p.R, nr, e + 2, make_double2(r[2], r[3]));
+        put(p.R, e, make_double2(r[0], r[1]));
+        put(p.R, e + 2, make_double2(r[2], r[3]));
         if (!(cflag & 4)) {
-            wt_put(p.wt & 8, p.Rh, (long long)p.k * p.ldr, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
-            wt_put(p.wt & 8, p.Rl, (long long)p.k * p.ldr, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+            put(p.Rh, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+            put(p.Rl, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
         }
-        panel_put_rexp(p, v, r);
     }
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, true);
 }
@@ -1759,20 +1214,14 @@ __global__ __launch_bounds__(kThreads) void k_panel_diag(PanelParams p, double* 
     const long long n = (long long)p.nblock * p.w;
     const long long col = (long long)blockIdx.x * 512 + lane * 8;
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float amax = 0.0f;
     for (long long i = wave; i < p.m && col < n; i += kWaves) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(p.A + i * p.lda + col);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const double d = (double)(float)v[e];
             acc[e] = fma(d, d, acc[e]);
-            amax = fmaxf(amax, fabsf((float)v[e]));
         }
     }
-    // max |A| for the e4m3 image of A (lo8): non-negative floats order as their bit patterns
-    amax = (float)wave_max((double)amax);
-    if (p.amax && lane == 0 && amax > 0.0f)
-        __hip_atomic_fetch_max(p.amax, __float_as_uint(amax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ double part[kWaves][512];
 #pragma unroll
     for (int e = 0; e < 8; ++e) part[wave][lane * 8 + e] = acc[e];
@@ -1781,99 +1230,6 @@ __global__ __launch_bounds__(kThreads) void k_panel_diag(PanelParams p, double* 
         const double s = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
         diag[blockIdx.x * 512 + c] = s;
         rec[blockIdx.x * 512 + c] = 1.0 / s;
-    }
-}
-
-// lo8: the exponent table of the residual p.R (reset and refresh; the update kernels keep it
-// current every iteration).  A thread owns 4 consecutive rows, a wave 256 rows of one RHS.
-__global__ __launch_bounds__(kThreads) void k_panel_rexp(PanelParams p) {
-    const unsigned ur = (unsigned)((long long)p.k * p.m / 4);
-    for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
-        const double2 r01 = *reinterpret_cast<const double2*>(p.R + 4ll * v);
-        const double2 r23 = *reinterpret_cast<const double2*>(p.R + 4ll * v + 2);
-        const double r[4] = {r01.x, r01.y, r23.x, r23.y};
-        panel_put_rexp(p, v, r);
-    }
-}
-
-// Exact residual refresh (lo8): the incremental R += gamma S drifts from B - A X by the e4m3 lo
-// product's error (S = A_hi D_hi + A8 D_lo8 != A D'), so every "r_refresh" iterations R is
-// recomputed from X.  X (fp32) = Xh + Xm + Xl exactly in three bf16 pieces (8 + 8 + 8 significant
-// bits); pass 2 multiplies (Xh, Xm) as its usual hi + lo pair and Xl as a one-piece operand, fp32
-// accumulation per column chunk, fp64 across chunks (k_panel_refresh_fin).
-__global__ __launch_bounds__(kThreads) void k_panel_xsplit3(PanelParams p, int block, __bf16* __restrict__ h,
-                                                            __bf16* __restrict__ m, __bf16* __restrict__ l) {
-    const long long nx = (long long)p.k * p.w;
-    for (long long e = (long long)blockIdx.x * kThreads + threadIdx.x; e < nx; e += (long long)gridDim.x * kThreads) {
-        const float x = p.X[(long long)block * nx + e];
-        const long long rhs = e / p.w;
-        const long long d = rhs * p.ldd + (e - rhs * p.w);
-        const __bf16 xh = to_bf16(x);
-        const float r1 = x - (float)xh;   // exact
-        const __bf16 xm = to_bf16(r1);
-        h[d] = xh;
-        m[d] = xm;
-        l[d] = to_bf16(r1 - (float)xm);   // exact: at most 8 significant bits remain
-    }
-}
-// acc = S (the (Xh, Xm) product, k_panel_reduce mode 0) + sum_c Sslab[c] (the Xl product);
-// one feature block: R = acc - B, its hi / lo split and exponent table; several: Ax_block = acc
-// (R then follows from all blocks, k_panel_r_from_ax).  A thread owns 4 consecutive rows.
-__global__ __launch_bounds__(kThreads) void k_panel_refresh_fin(PanelParams p, int block) {
-    const long long nr = (long long)p.k * p.m;
-    const unsigned ur = (unsigned)(nr / 4), m4 = (unsigned)(p.m / 4);
-    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-    for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
-        const long long e = 4ll * v;
-        double a[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] = p.S[e + q];
-        for (int c = 0; c < p.kchunks; ++c) {
-            const float4 s = *reinterpret_cast<const float4*>(p.Sslab + (long long)c * nr + e);
-            a[0] += (double)s.x; a[1] += (double)s.y; a[2] += (double)s.z; a[3] += (double)s.w;
-        }
-        if (p.nblock == 1) {
-            const unsigned rhs = v / m4;
-            const long long re = (long long)rhs * p.ldr + (e - (long long)rhs * p.m);
-            double r[4];
-            __bf16 hi[4], lo[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                r[q] = a[q] - p.B[e + q];
-                split_bf16(r[q], hi[q], lo[q]);
-                p.R[e + q] = r[q];
-            }
-            *reinterpret_cast<bf16x4v*>(p.Rh + re) = bf16x4v{hi[0], hi[1], hi[2], hi[3]};
-            *reinterpret_cast<bf16x4v*>(p.Rl + re) = bf16x4v{lo[0], lo[1], lo[2], lo[3]};
-            panel_put_rexp(p, v, r);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) p.Ax[(long long)block * nr + e + q] = a[q];
-        }
-    }
-}
-// several feature blocks, after every block's refresh: R = sum_b Ax_b - B, split, exponent table
-__global__ __launch_bounds__(kThreads) void k_panel_r_from_ax(PanelParams p) {
-    const long long nr = (long long)p.k * p.m;
-    const unsigned ur = (unsigned)(nr / 4), m4 = (unsigned)(p.m / 4);
-    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-    for (unsigned v = blockIdx.x * kThreads + threadIdx.x; v < ur; v += gridDim.x * kThreads) {
-        const long long e = 4ll * v;
-        const unsigned rhs = v / m4;
-        const long long re = (long long)rhs * p.ldr + (e - (long long)rhs * p.m);
-        double r[4];
-        __bf16 hi[4], lo[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            double acc = p.Ax[e + q];
-            for (int b = 1; b < p.nblock; ++b) acc += p.Ax[(long long)b * nr + e + q];
-            r[q] = acc - p.B[e + q];
-            split_bf16(r[q], hi[q], lo[q]);
-            p.R[e + q] = r[q];
-        }
-        *reinterpret_cast<bf16x4v*>(p.Rh + re) = bf16x4v{hi[0], hi[1], hi[2], hi[3]};
-        *reinterpret_cast<bf16x4v*>(p.Rl + re) = bf16x4v{lo[0], lo[1], lo[2], lo[3]};
-        panel_put_rexp(p, v, r);
     }
 }
 

@@ -33,30 +33,22 @@ struct bpgl_panel {
     int64_t timed_iters = 0;
     bool kind_used[kPanelKinds] = {};   // kinds recorded in the current window (step: folded into reduce)
     int interleave[2] = {2, -1};  // mainloop variant per pass (tuning knobs; -1: the measured default, panel_ilv)
-    int waves[2] = {0, 0};        // waves along the RHS per pass: 0 = 2 (8 waves), 4 = 16 waves ("waves" knobs)
     int dsplit = 1;               // bf16 pieces of the solver's direction (d_split knob; 1 since round 4)
-    int wt = 0;                   // write-through store sites ("write_through" knob, PanelParams::wt)
     int defer_x = 1;              // one block: x += gamma D' in the next pass-1 epilogue ("defer_x" knob; round 4 default)
-    int64_t op_pad = 0;           // bf16 elements appended to every RHS row of the operand images ("op_pad" knob, before bind)
     int carry_g = 1;              // carried gradient, one feature block ("carry_g" knob; ignored for nblock > 1)
     int64_t g_period = 64;        // exact gradient every g_period iterations ("g_refresh" knob)
     int gm_cur = 0;               // pass-1 form of the launch being enqueued: 0 plain, 1 exact + store G, 2 carried
     hipGraphExec_t gexec_ref = nullptr;   // carry_g: a graph whose first iteration is the exact-gradient one
-    int lo8 = 0;                  // e4m3 lo products ("lo8" knob): bit 0 pass 1 (residual), bit 1 pass 2 (direction)
-    int64_t r_period = 128;       // exact residual refresh every r_period iterations when pass 2 runs lo8 ("r_refresh")
     int64_t t_host = 0;           // iterations enqueued since the last reset
-    int64_t last_refresh = 0;     // t_host of the last refresh
-    int64_t n_refresh = 0;        // refreshes since the last reset
     int64_t n_exact = 0;          // carried gradient: exact-gradient iterations since the last reset
-    int64_t ldr() const { return m + op_pad; }
-    int64_t ldd() const { return w + op_pad; }
+    int64_t ldr() const { return m; }
+    int64_t ldd() const { return w; }
 };
 
 namespace {
 
 struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, amax, rexp, dexp,
-        X3, Gc, Sh, Ec, total;
+    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, Gc, Sh, Ec, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -81,33 +73,17 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.gamma = k.take(8 * c->k);
     L.err_rhs = k.take(8 * c->k);
     L.cnt = k.take(8 * (int64_t)c->k);
-    L.amax = k.take(8);
-    L.rexp = k.take(4 * (int64_t)c->k * (c->m / kPanelRows));
-    L.dexp = k.take(4 * (c->w / kPanelRows) * (int64_t)c->k);
-    L.X3 = k.take(2 * (int64_t)c->k * c->ldd());   // the third bf16 piece of X (residual refresh)
-    L.Gc = k.take(4 * kw);                           // the carried gradient (fp32)
-    L.Sh = k.take(2 * (int64_t)c->k * c->ldr());     // the carried product's bf16 operand
-    L.Ec = k.take(4 * km);                           // its rounding error, fed into the next one (fp32)
+    // the carried gradient's state (one feature block only; ADVICE r04: not reserved otherwise)
+    const bool carry = c->nblock == 1;
+    L.Gc = k.take(carry ? 4 * kw : 0);                           // the carried gradient (fp32)
+    L.Sh = k.take(carry ? 2 * (int64_t)c->k * c->ldr() : 0);     // the carried product's bf16 operand
+    L.Ec = k.take(carry ? 4 * km : 0);                           // its rounding error, fed into the next one (fp32)
     L.total = k.off;
     return L;
 }
 
 // ns: bf16 pieces of the direction (pass 1's epilogue writes it, pass 2 reads it): the
 // solver's d_split knob, 2 for the API products (bpgl_panel_mtm / _mm)
-// lo8 forms: 8 waves (WNX 0); mainloop ILV 0, 1 or 2 (the staggered form 3 falls back to 2)
-template <int NT, int NS, int ILV>
-int panel_launch_lo8_ilv(bpgl_panel* c, int which) {
-    if (which == 0) {
-        hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
-                           dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1, nullptr);
-        LAUNCH_CHECK("k_panel_pass1");
-    } else {
-        const dim3 g((unsigned)((c->m / kPanelRows) * c->kchunks));
-        hipLaunchKernelGGL((k_panel_pass2<NT, ILV, 2, 0, 1>), g, dim3(PanelGeo<NT, 2, 0>::T), 0, c->stream, c->p, -1);
-        LAUNCH_CHECK("k_panel_pass2");
-    }
-    return 0;
-}
 // the mainloop variant of a pass: the knob, or the measured default -- pass 1: 2 (software-pipelined);
 // pass 2: 2 with the bf16 direction alone at k >= 64 (+0.7 % at k = 64 and 128), else 1 (k = 32 and the
 // hi + lo direction; profiles/r04/ilv)
@@ -116,81 +92,53 @@ int panel_ilv(const bpgl_panel* c, int which, int ns) {
     if (v >= 0) return v;
     return which == 0 ? 2 : (ns == 1 && c->k >= 64 ? 2 : 1);
 }
-template <int NT, int NS>
-int panel_launch_lo8(bpgl_panel* c, int which) {
-    switch (panel_ilv(c, which, NS)) {
-        case 0: return panel_launch_lo8_ilv<NT, NS, 0>(c, which);
-        case 1: return panel_launch_lo8_ilv<NT, NS, 1>(c, which);
-        default: return panel_launch_lo8_ilv<NT, NS, 2>(c, which);
-    }
-}
-template <int NS>
-int panel_launch_lo8_ns(bpgl_panel* c, int which) {
-    switch (c->k) {
-        case 16: return panel_launch_lo8<1, NS>(c, which);
-        case 32: return panel_launch_lo8<2, NS>(c, which);
-        case 64: return panel_launch_lo8<4, NS>(c, which);
-        default: return panel_launch_lo8<8, NS>(c, which);
-    }
-}
-
-template <int NT, int ILV, int NS, int WNX>
+template <int NT, int ILV, int NS>
 int panel_launch_nt(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (which) {
         case 0:
             {   // carried-gradient forms (one feature block)
                 if (mode && c->gm_cur == 1) {
-                    hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX, 0, 1>), dim3((unsigned)(c->w / kPanelRows)),
-                                       dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+                    hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, 1>), dim3((unsigned)(c->w / kPanelRows)),
+                                       dim3(PanelGeo<NT, 2>::T), 0, c->stream, c->p, fixed_block, out);
                     LAUNCH_CHECK("k_panel_pass1");
                     break;
                 }
                 if (mode && c->gm_cur == 2) {
-                    hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX, 0, 2>), dim3((unsigned)(c->w / kPanelRows)),
-                                       dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+                    hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, 2>), dim3((unsigned)(c->w / kPanelRows)),
+                                       dim3(PanelGeo<NT, 2>::T), 0, c->stream, c->p, fixed_block, out);
                     LAUNCH_CHECK("k_panel_pass1");
                     break;
                 }
             }
-            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS, WNX>), dim3((unsigned)(c->w / kPanelRows)),
-                                         dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
-            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2, WNX>), dim3((unsigned)(c->w / kPanelRows)),
-                                    dim3(PanelGeo<NT, 2, WNX>::T), 0, c->stream, c->p, fixed_block, out);
+            if (mode) hipLaunchKernelGGL((k_panel_pass1<NT, 1, ILV, NS>), dim3((unsigned)(c->w / kPanelRows)),
+                                         dim3(PanelGeo<NT, 2>::T), 0, c->stream, c->p, fixed_block, out);
+            else hipLaunchKernelGGL((k_panel_pass1<NT, 0, ILV, 2>), dim3((unsigned)(c->w / kPanelRows)),
+                                    dim3(PanelGeo<NT, 2>::T), 0, c->stream, c->p, fixed_block, out);
             LAUNCH_CHECK("k_panel_pass1");
             break;
         case 1:
-            hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS, WNX>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
-                               dim3(PanelGeo<NT, NS, WNX>::T), 0, c->stream, c->p, fixed_block);
+            hipLaunchKernelGGL((k_panel_pass2<NT, ILV, NS>), dim3((unsigned)((c->m / kPanelRows) * c->kchunks)),
+                               dim3(PanelGeo<NT, NS>::T), 0, c->stream, c->p, fixed_block);
             LAUNCH_CHECK("k_panel_pass2");
             break;
     }
     return 0;
 }
-template <int NT, int NS, int WNX>
+template <int NT, int NS>
 int panel_launch_ilv(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (panel_ilv(c, which, NS)) {
-        case 0: return panel_launch_nt<NT, 0, NS, WNX>(c, which, fixed_block, out, mode);
-        case 1: return panel_launch_nt<NT, 1, NS, WNX>(c, which, fixed_block, out, mode);
-        case 2: return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
-        default:
-            if constexpr (NT == 8 && WNX == 0) return panel_launch_nt<NT, 3, NS, WNX>(c, which, fixed_block, out, mode);
-            else return panel_launch_nt<NT, 2, NS, WNX>(c, which, fixed_block, out, mode);
+        case 0: return panel_launch_nt<NT, 0, NS>(c, which, fixed_block, out, mode);
+        case 1: return panel_launch_nt<NT, 1, NS>(c, which, fixed_block, out, mode);
+        default: return panel_launch_nt<NT, 2, NS>(c, which, fixed_block, out, mode);
     }
-}
-template <int NT, int NS>
-int panel_launch_wn(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
-    if constexpr (NT >= 4) {
-        if (c->waves[which] == 4) return panel_launch_ilv<NT, NS, 4>(c, which, fixed_block, out, mode);
-    }
-    return panel_launch_ilv<NT, NS, 0>(c, which, fixed_block, out, mode);
 }
 template <int NS>
 int panel_launch_ns(bpgl_panel* c, int which, int fixed_block, double* out, int mode) {
     switch (c->k) {
-        case 16: return panel_launch_wn<1, NS>(c, which, fixed_block, out, mode);
-        case 32: return panel_launch_wn<2, NS>(c, which, fixed_block, out, mode);
-        case 64: return panel_launch_wn<4, NS>(c, which, fixed_block, out, mode);
-        default: return panel_launch_wn<8, NS>(c, which, fixed_block, out, mode);
+        case 16: return panel_launch_ilv<1, NS>(c, which, fixed_block, out, mode);
+        case 32: return panel_launch_ilv<2, NS>(c, which, fixed_block, out, mode);
+        case 64: return panel_launch_ilv<4, NS>(c, which, fixed_block, out, mode);
+        default: return panel_launch_ilv<8, NS>(c, which, fixed_block, out, mode);
     }
 }
 int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mode, int ns) {
@@ -198,13 +146,7 @@ int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mod
                    : panel_launch_ns<2>(c, which, fixed_block, out, mode);
 }
 bool panel_carry(const bpgl_panel* c) { return c->carry_g && c->nblock == 1; }
-// a solver pass: the lo8 form when the knob selects it for this pass (pass 2 needs the hi + lo direction)
-int panel_pass(bpgl_panel* c, int which) {
-    if (which == 0 && c->gm_cur) return panel_launch(c, 0, -1, nullptr, 1, c->dsplit);   // carried gradient
-    const bool l8 = which == 0 ? (c->lo8 & 1) != 0 : ((c->lo8 & 2) != 0 && c->dsplit == 2);
-    if (l8) return c->dsplit == 1 ? panel_launch_lo8_ns<1>(c, which) : panel_launch_lo8_ns<2>(c, which);
-    return panel_launch(c, which, -1, nullptr, 1, c->dsplit);
-}
+int panel_pass(bpgl_panel* c, int which) { return panel_launch(c, which, -1, nullptr, 1, c->dsplit); }
 int panel_reduce(bpgl_panel* c, double* out, int mode) {
     hipLaunchKernelGGL(k_panel_reduce, dim3((unsigned)(c->k * cdiv(c->m, kLspRows))), dim3(kThreads), 0, c->stream,
                        c->p, out, mode);
@@ -271,51 +213,6 @@ int panel_split(bpgl_panel* c, const double* src, int64_t len, int64_t ld, __bf1
     LAUNCH_CHECK("k_panel_split");
     return 0;
 }
-// exact residual refresh (lo8 in pass 2; bpgl_panel.h k_panel_xsplit3): R = A X - B from X's three
-// bf16 pieces, per feature block, then the residual's split and exponent table
-int panel_refresh(bpgl_panel* c) {
-    PanelParams& p = c->p;
-    const int64_t nx = (int64_t)c->k * c->w, nr = (int64_t)c->k * c->m;
-    if (c->defer_x) {   // x += gamma D' of the last iteration first: X must be current
-        const dim3 fg((unsigned)std::min<int64_t>(cdiv(nx / 8, kThreads), 8192));
-        if (c->dsplit == 1) hipLaunchKernelGGL(k_panel_flush<1>, fg, dim3(kThreads), 0, c->stream, p);
-        else hipLaunchKernelGGL(k_panel_flush<2>, fg, dim3(kThreads), 0, c->stream, p);
-        LAUNCH_CHECK("k_panel_flush");
-        hipLaunchKernelGGL(k_panel_clear_pending, dim3(1), dim3(64), 0, c->stream, p);
-        LAUNCH_CHECK("k_panel_clear_pending");
-    }
-    __bf16* x3 = (__bf16*)((char*)p.st + (panel_layout(c).X3 - panel_layout(c).st));
-    const dim3 eg((unsigned)std::min<int64_t>(cdiv(nx, kThreads), 8192));
-    const dim3 rg((unsigned)std::min<int64_t>(cdiv(nr / 4, kThreads), 8192));
-    int rc;
-    for (int b = 0; b < c->nblock; ++b) {
-        hipLaunchKernelGGL(k_panel_xsplit3, eg, dim3(kThreads), 0, c->stream, p, b, p.Dh, p.Dl, x3);
-        LAUNCH_CHECK("k_panel_xsplit3");
-        if ((rc = panel_launch(c, 1, b, nullptr, 0, 2))) return rc;   // (Xh, Xm) -> slab
-        if ((rc = panel_reduce(c, p.S, 0))) return rc;                // -> S
-        __bf16* dh = p.Dh;
-        p.Dh = x3;                                                    // Xl alone -> slab
-        rc = panel_launch(c, 1, b, nullptr, 0, 1);
-        p.Dh = dh;
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_panel_refresh_fin, rg, dim3(kThreads), 0, c->stream, p, b);
-        LAUNCH_CHECK("k_panel_refresh_fin");
-    }
-    if (c->nblock > 1) {
-        hipLaunchKernelGGL(k_panel_r_from_ax, rg, dim3(kThreads), 0, c->stream, p);
-        LAUNCH_CHECK("k_panel_r_from_ax");
-    }
-    c->n_refresh++;
-    c->last_refresh = c->t_host;
-    return 0;
-}
-int panel_rexp(bpgl_panel* c) {
-    const dim3 rg((unsigned)std::min<int64_t>(cdiv((int64_t)c->k * c->m / 4, kThreads), 8192));
-    hipLaunchKernelGGL(k_panel_rexp, rg, dim3(kThreads), 0, c->stream, c->p);
-    LAUNCH_CHECK("k_panel_rexp");
-    return 0;
-}
-
 void drop_graphs(bpgl_panel* c) {
     if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
     if (c->gexec_ref) { (void)hipGraphExecDestroy(c->gexec_ref); c->gexec_ref = nullptr; }
@@ -342,7 +239,7 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
                                               kPanelRows);
     if (w <= 0 || w % kPanelRows) return fail(BPGL_E_ARG, "block width (%lld) must be a positive multiple of %d",
                                               (long long)w, kPanelRows);
-    if (kchunks <= 0) {   // one pass-2 tile per CU (256), chunk width a multiple of two 64-deep stages (lo8)
+    if (kchunks <= 0) {   // one pass-2 tile per CU (256), chunk width a multiple of two 64-deep stages
         kchunks = (int32_t)std::max<int64_t>(1, std::min<int64_t>(w / (2 * kPanelK), 256 / (m / kPanelRows)));
         while (kchunks > 1 && w % ((int64_t)kchunks * 2 * kPanelK)) --kchunks;
     }
@@ -422,12 +319,8 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.gamma = (double*)(s + L.gamma);
     p.err_rhs = (double*)(s + L.err_rhs);
     p.cnt = (unsigned long long*)(s + L.cnt);
-    p.amax = (unsigned*)(s + L.amax);
     p.Gc = (float*)(s + L.Gc);
     p.Ec = (float*)(s + L.Ec);
-    p.rexp = (int*)(s + L.rexp);
-    p.dexp = (int*)(s + L.dexp);
-    p.wt = c->wt;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
     c->bound = true;
@@ -441,7 +334,6 @@ int bpgl_panel_diag(bpgl_panel* c, double* out) {
     int rc;
     if ((rc = panel_ready(c))) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(c->p.amax, 0, sizeof(unsigned), c->stream));
     hipLaunchKernelGGL(k_panel_diag, dim3((unsigned)cdiv(c->n, 512)), dim3(kThreads), 0, c->stream, c->p,
                        const_cast<double*>(c->p.diag), const_cast<double*>(c->p.rec));
     LAUNCH_CHECK("k_panel_diag");
@@ -488,10 +380,7 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     HIP_TRY(hipMemsetAsync(p.Ax, 0, 8 * km * c->nblock, c->stream));
     // x = 0 => Ax = 0, R = -B
     if ((rc = panel_split(c, p.B, c->m, c->ldr(), p.Rh, p.Rl, -1.0, p.R))) return rc;
-    if ((rc = panel_rexp(c))) return rc;
     c->t_host = 0;
-    c->last_refresh = 0;
-    c->n_refresh = 0;
     c->n_exact = 0;
     p.err_iter = err_iter;
     p.rec_len = err_iter ? record_len : 0;
@@ -535,24 +424,17 @@ int bpgl_panel_step(bpgl_panel* c, int64_t n_iter) {
     if ((rc = panel_ready(c))) return rc;
     if (!c->solver) return fail(BPGL_E_STATE, "bpgl_panel_reset has not been called");
     HIP_TRY(hipSetDevice(c->device));
-    // lo8 in pass 2: an exact residual refresh every r_period iterations (between graph replays;
-    // r_period is a multiple of the graph length, so no replay crosses one)
-    const bool refresh = (c->lo8 & 2) && c->dsplit == 2 && c->r_period > 0;
     int64_t i = 0;
     while (i < n_iter) {
-        if (refresh && c->t_host > 0 && c->t_host % c->r_period == 0 && c->last_refresh != c->t_host)
-            if ((rc = panel_refresh(c))) return rc;
-        // carried gradient: every g_period-th iteration (the first included) computes G exactly, and so
-        // does the first one after a residual refresh (R jumped to A X - B; G follows it)
-        const bool exact = panel_carry(c) && (c->t_host % c->g_period == 0 || c->last_refresh == c->t_host);
+        // carried gradient: every g_period-th iteration (the first included) computes G exactly
+        const bool exact = panel_carry(c) && c->t_host % c->g_period == 0;
         if (!c->timing && c->gexec && i + kGraphIters <= n_iter && c->t_host % kGraphIters == 0) {
             HIP_TRY(hipGraphLaunch(exact ? c->gexec_ref : c->gexec, c->stream));
             c->n_exact += exact;
             i += kGraphIters;
             c->t_host += kGraphIters;
         } else {
-            const bool next_exact = (c->t_host + 1) % c->g_period == 0 ||
-                                    (refresh && (c->t_host + 1) % c->r_period == 0);
+            const bool next_exact = (c->t_host + 1) % c->g_period == 0;
             if ((rc = panel_iteration(c, c->timing ? c->timed_iters : 0, exact, next_exact || i + 1 == n_iter)))
                 return rc;
             c->n_exact += exact;
@@ -617,18 +499,9 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
     if (!c || !key) return fail(BPGL_E_ARG, "null argument");
     const bool both = !strcmp(key, "interleave");
     if (both || !strcmp(key, "interleave1") || !strcmp(key, "interleave2")) {
-        if (value < 0 || value > 3) return fail(BPGL_E_ARG, "interleave must be 0, 1, 2 or 3");
+        if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
-    } else if (!strcmp(key, "waves") || !strcmp(key, "waves1") || !strcmp(key, "waves2")) {
-        if (value != 0 && value != 4) return fail(BPGL_E_ARG, "waves must be 0 (8 waves per block) or 4 (16 waves)");
-        if (value == 4 && c->k < 64) return fail(BPGL_E_ARG, "waves = 4 needs nrhs >= 64");
-        if (key[5] != '2') c->waves[0] = (int)value;
-        if (key[5] != '1') c->waves[1] = (int)value;
-    } else if (!strcmp(key, "write_through")) {
-        if (value < 0 || value > 15) return fail(BPGL_E_ARG, "write_through is a mask of 4 bits");
-        c->wt = (int)value;
-        c->p.wt = c->wt;
     } else if (!strcmp(key, "defer_x")) {
         if (value != 0 && value != 1) return fail(BPGL_E_ARG, "defer_x must be 0 or 1");
         c->defer_x = (int)value;
@@ -646,26 +519,6 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
             return fail(BPGL_E_ARG, "g_refresh must be a positive multiple of %d", kGraphIters);
         c->g_period = value;
         c->solver = false;
-    } else if (!strcmp(key, "lo8")) {
-        if (value < 0 || value > 3) return fail(BPGL_E_ARG, "lo8 is a mask: 1 pass 1 (residual), 2 pass 2 (direction)");
-        if ((value & 2) && (c->w / c->kchunks) % (2 * kPanelK))
-            return fail(BPGL_E_ARG, "lo8 in pass 2 needs a column chunk (w / kchunks) that is a multiple of %d",
-                        2 * kPanelK);
-        c->lo8 = (int)value;
-        c->solver = false;   // the refresh schedule restarts with the solve: a reset must follow
-    } else if (!strcmp(key, "r_refresh")) {
-        if (value < 0 || value % kGraphIters)
-            return fail(BPGL_E_ARG, "r_refresh must be 0 (never) or a positive multiple of %d", kGraphIters);
-        c->r_period = value;
-        return 0;
-    } else if (!strcmp(key, "op_pad")) {   // changes the scratch layout: only before bpgl_panel_bind
-        if (c->bound) return fail(BPGL_E_STATE, "op_pad must be set before bpgl_panel_bind");
-        if (value < 0 || value % 64 || value > 4096)
-            return fail(BPGL_E_ARG, "op_pad must be a multiple of 64 in [0, 4096] (bf16 elements)");
-        if ((int64_t)c->k * (c->w + value) >= (1ll << 31) || (int64_t)c->k * (c->m + value) >= (1ll << 31))
-            return fail(BPGL_E_ARG, "nrhs * (width + op_pad) must stay below 2^31");
-        c->op_pad = value;
-        return 0;
     } else {
         return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     }
@@ -678,37 +531,22 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     if (!strcmp(key, "interleave1")) *value = panel_ilv(c, 0, c->dsplit);
     else if (!strcmp(key, "interleave2")) *value = panel_ilv(c, 1, c->dsplit);   // the solver's pass 2
     else if (!strcmp(key, "d_split")) *value = c->dsplit;
-    else if (!strcmp(key, "waves1")) *value = c->waves[0];
-    else if (!strcmp(key, "waves2")) *value = c->waves[1];
-    else if (!strcmp(key, "write_through")) *value = c->wt;
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
-    else if (!strcmp(key, "op_pad")) *value = c->op_pad;
-    else if (!strcmp(key, "lo8")) *value = c->lo8;
     else if (!strcmp(key, "carry_g")) *value = panel_carry(c) ? 1 : 0;   // the form in effect
     else if (!strcmp(key, "g_refresh")) *value = c->g_period;
-    else if (!strcmp(key, "r_refresh")) *value = c->r_period;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);
     return 0;
 }
 
 int bpgl_panel_stat(const bpgl_panel* c, const char* key, int64_t* value) {
     if (!c || !key || !value) return fail(BPGL_E_ARG, "null argument");
-    if (!strcmp(key, "refreshes")) *value = c->n_refresh;
-    else if (!strcmp(key, "iters_enqueued")) *value = c->t_host;
+    if (!strcmp(key, "iters_enqueued")) *value = c->t_host;
     else if (!strcmp(key, "exact_gradients")) *value = c->n_exact;
     else return fail(BPGL_E_ARG, "unknown panel stat '%s'", key);
     return 0;
 }
 
 const double* bpgl_panel_residual(bpgl_panel* c) { return c ? c->p.R : nullptr; }
-
-int bpgl_panel_refresh(bpgl_panel* c) {
-    int rc;
-    if ((rc = panel_ready(c))) return rc;
-    if (!c->solver) return fail(BPGL_E_STATE, "bpgl_panel_reset has not been called");
-    HIP_TRY(hipSetDevice(c->device));
-    return panel_refresh(c);
-}
 
 int bpgl_panel_geometry(const bpgl_panel* c, int32_t* kchunks) {
     if (!c) return fail(BPGL_E_ARG, "null panel context");

@@ -7,16 +7,25 @@ GEMVs, then applies the reference's shrink, exact line search and update to
 every right-hand side (cyclic block order, fixed iteration count).
 
 Numerics (stated tolerance): A is stored as bf16 (the problem is defined by the
-bf16-rounded A); the residual enters the MFMA as a hi + lo bf16 pair, the
-direction as its bf16 rounding (d_split = 1, the default) or as a hi + lo pair
-(d_split = 2), with fp32 accumulation per block tile and fp64 after that.  The
-line search is exact along the direction the MFMA saw, so both forms converge to
-the same solution, which the gradient pass (hi + lo) fixes.  Against the fp64
-oracle on the same bf16 A: after the reference's 1000 iterations at the full
-configs[4] shape x within 1e-4 relative l2 (measured 1.7-2.2e-5 for both forms)
-and the objective within 1e-5 (measured ~1e-11) (tests/test_longrun.py); over
-short runs, where the two forms' trajectories differ, x within 1e-2 and the
-objective within 1e-5 (tests/test_panel.py).
+bf16-rounded A); fp32 accumulation per block tile, fp64 after that.  The default
+path (one feature block) is:
+
+* the direction enters the A D pass as its bf16 rounding (d_split = 1; 2 = a
+  hi + lo bf16 pair), and the line search is exact along the direction the MFMA
+  saw, so every step is an exact line search (monotone objective);
+* the gradient is carried (carry_g = 1): G_t = G_{t-1} + gamma A^T bf16(V) in
+  fp32, with V = gamma S + the previous rounding (error feedback), and computed
+  exactly from the residual's hi + lo bf16 pair every g_refresh = 64 iterations;
+* x += gamma D' is applied by the next pass-1 epilogue (defer_x = 1; bitwise the
+  same x).
+
+Against the fp64 oracle on the same bf16 A: after the reference's 1000
+iterations at the full configs[4] shape, x within 1e-4 relative l2 (measured
+3.6-4.1e-6 for the default, 1.7-2.2e-5 for the exact-gradient forms) and the
+objective within 1e-5 (measured ~1e-12) (tests/test_longrun.py).  Over short
+runs the forms follow different trajectories to the same fixed point: x within
+1e-2 and the objective within 1e-4 on the default path (tests/test_panel.py;
+1e-5 for the exact-gradient hi + lo form).
 
 All compute goes through libbpgl.so (bpgl_panel_* in include/bpgl.h).
 """
@@ -50,7 +59,6 @@ _PANEL_SIGS = {
     "bpgl_panel_get_tuning": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(_i64)]),
     "bpgl_panel_stat": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(_i64)]),
     "bpgl_panel_residual": (_p, [_p]),
-    "bpgl_panel_refresh": (ctypes.c_int, [_p]),
 }
 N._SIGS.update(_PANEL_SIGS)
 
@@ -68,10 +76,7 @@ class PanelLasso:
 
     KERNEL_KINDS = ("pass1_mfma", "pass2_mfma", "reduce", "step", "update")
 
-    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0, op_pad=0, lda_pad=0):
-        """op_pad: bf16 elements appended to each right-hand side's row of the residual / direction
-        images (a multiple of 64; layout only, bitwise-identical results).  lda_pad: columns appended to
-        each row of the stored bf16 A (a multiple of 8; the padding is never read)."""
+    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0):
         L = _lib()
         self.Block = int(Block)
         self.nrhs = int(nrhs)
@@ -88,18 +93,11 @@ class PanelLasso:
         N.check(L.bpgl_panel_create(ctypes.byref(ctx), self.device.index, H, K, self.Block, self.nrhs,
                                     int(kchunks), ctypes.c_void_p(self.stream.cuda_stream)), "bpgl_panel_create")
         self._ctx = ctx
-        if op_pad:
-            N.check(L.bpgl_panel_set_tuning(ctx, b"op_pad", int(op_pad)), "bpgl_panel_set_tuning(op_pad)")
-        lda = K + int(lda_pad)
+        lda = K
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             A_src = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))
-            if lda_pad:
-                self._A_store = torch.zeros((H, lda), dtype=torch.bfloat16, device=self.device)
-                self._A_store[:, :K].copy_(A_src.to(device=self.device, dtype=torch.bfloat16))
-                self._A = self._A_store[:, :K]                                                 # [m][n], row pitch lda
-            else:
-                self._A = A_src.to(device=self.device, dtype=torch.bfloat16).contiguous()     # [m][n]
+            self._A = A_src.to(device=self.device, dtype=torch.bfloat16).contiguous()     # [m][n]
             nbytes = int(L.bpgl_panel_scratch_bytes(ctx))
             self._scratch = torch.empty(nbytes // 8 + 64, dtype=torch.float64, device=self.device)
             base = (self._scratch.data_ptr() + 255) // 256 * 256
@@ -194,11 +192,15 @@ class PanelLasso:
         return self.solver_x_device().to(torch.float64).cpu().numpy().T.copy()   # (n, k)
 
     def set_tuning(self, key, value):
-        """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave' 0-2.
-        'd_split' 1 (default) / 2: the solver's direction enters the A D pass as its bf16 rounding (1)
-        or as a hi + lo pair (2); both are exact line searches along the direction taken.  'lo8' (mask,
-        opt-in) / 'r_refresh': e4m3 lo products; 'carry_g' (default 1, one block) / 'g_refresh': the
-        carried fp32 gradient with an exact recompute every g_refresh iterations (include/bpgl.h)."""
+        """Speed-only knobs (bitwise-identical results): 'interleave1' / 'interleave2' / 'interleave'
+        0-2 (the mainloop form; default: the measured best per pass); 'defer_x' 0 / 1 (default 1, one
+        block: where x += gamma D' is applied; a reset must follow).
+
+        Knobs that change the arithmetic (each an exact line search along the direction taken; the
+        accuracy of each against the oracle is in the module docstring): 'd_split' 1 (default) / 2 --
+        the direction as its bf16 rounding or a hi + lo pair; 'carry_g' 1 (default, one block) / 0 --
+        the carried fp32 gradient or the exact A^T R product every iteration; 'g_refresh' (default 64,
+        a multiple of 8) -- the carried gradient's exact recompute period (include/bpgl.h)."""
         N.check(_lib().bpgl_panel_set_tuning(self._ctx, key.encode(), int(value)), "bpgl_panel_set_tuning")
 
     def get_tuning(self, key):
@@ -207,7 +209,7 @@ class PanelLasso:
         return v.value
 
     def stat(self, key):
-        """Counter since the last reset: "refreshes", "iters_enqueued", "exact_gradients"."""
+        """Counter since the last reset: "iters_enqueued", "exact_gradients"."""
         v = ctypes.c_int64()
         N.check(_lib().bpgl_panel_stat(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_panel_stat")
         return v.value
@@ -218,11 +220,6 @@ class PanelLasso:
         off = addr - self._scratch.data_ptr()
         assert off % 8 == 0
         return self._scratch[off // 8: off // 8 + self.nrhs * self.MAT_HEIGHT].view(self.nrhs, self.MAT_HEIGHT)
-
-    def refresh(self):
-        """Recompute the residual exactly from X (the lo8 refresh) now."""
-        with self._on_stream():
-            N.check(_lib().bpgl_panel_refresh(self._ctx), "bpgl_panel_refresh")
 
     def set_kernel_timing(self, enable):
         N.check(_lib().bpgl_panel_set_kernel_timing(self._ctx, int(bool(enable))), "bpgl_panel_set_kernel_timing")

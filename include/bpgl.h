@@ -58,8 +58,12 @@ const char* bpgl_last_error(void);
  *   200 (0.2.0): + bpgl_stream_create / bpgl_stream_destroy; bpgl_iterate always synchronises
  *                the solver stream before returning; the "onepass_cache_permille" default moved
  *                from 0 to -1 (automatic: 750 when the rank's A block fits the Infinity Cache);
- *                panel tuning keys "lo8" (e4m3 lo products), "r_refresh", "carry_g"
- *                (default 1: the carried gradient, one feature block) and "g_refresh". */
+ *                panel tuning keys "carry_g" (default 1: the carried gradient, one feature
+ *                block) and "g_refresh".
+ *   300 (0.3.0): the opt-in forms measured to lose were removed:
+ *                tuning keys "fused", "onepass_fold", "onepass_variant"; panel keys "lo8",
+ *                "r_refresh", "write_through", "op_pad", "waves*", interleave 3; panel stat
+ *                "refreshes"; bpgl_panel_refresh. */
 int bpgl_version(void);
 
 /*
@@ -261,20 +265,15 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  * each path is bitwise deterministic):
  *   "onepass" (default -1 = when eligible, 0 = off, 1 = required): one pass
  *   over A per iteration, the gradient carried as g += gamma A^T (A D); needs
- *   one feature block, one rank (or row shards), no fused mode, at most
+ *   one feature block, one rank (or row shards), at most
  *   128 x 4096 columns (fp32; 128 x 6144 for bf16, 128 x 2048 for fp64) and all
  *   of its blocks resident at once (nothing else running on the device).
  *   "onepass_cache_permille" (default -1 = auto: 750 when this rank's A block is
  *   at most 320 MiB, i.e. about the 256 MiB Infinity Cache, else 0): share of every
  *   row group the one-pass kernel reads with cache-allocating loads (launches
  *   alternate the row direction, so the next launch starts on those rows).
- *   "onepass_fold" (default 0): 1 sums the row groups' U partials inside k_onepass
- *   (write-through partials + a per-segment barrier) instead of in k_onepass_fold
- *   (row shards) / k_onepass_tail (one rank) -- measured slower, kept as an option.
- *   "onepass_variant" (default 0, 0-3): register-ring depth / prefetch distance.
  *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
- *   "fused" (default 0): the two-launch fused iteration.
  *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for
  *   a caller-side exchange): row shards' per-iteration exchange in fp32 -- half the
  *   bytes, x within 2e-7 (1 rank) to 1.5e-6 (8 ranks) of the fp64 exchange.
@@ -322,11 +321,10 @@ int bpgl_panel_set_kernel_timing(bpgl_panel* ctx, int enable);
 int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, reduce (+ line search), step (0: folded into reduce), update */,
                             int64_t* samples);
 /* tuning knobs.  Results are bitwise independent of these: "interleave1",
- * "interleave2" (pass 1 / pass 2; "interleave" sets both) 0/1/2/3 -- LDS-DMA
+ * "interleave2" (pass 1 / pass 2; "interleave" sets both) 0/1/2 -- LDS-DMA
  * pieces issued together after each stage barrier (0), spread over the stage's
  * MFMA groups (1), or spread and software-pipelined with fragment reads one MFMA
- * group ahead across the stage barrier (2), or (3, k = 128) the staggered
- * four-phase form.  Defaults: pass 1 -- 2; pass 2 -- 2 with the bf16 direction
+ * group ahead across the stage barrier (2).  Defaults: pass 1 -- 2; pass 2 -- 2 with the bf16 direction
  * (d_split 1) at k >= 64, else 1 (round 4); get_tuning reports the form in use.
  * This one selects the solver's arithmetic (every choice is an exact line
  * search along the direction it takes): "d_split" 1 (default since ABI 200) --
@@ -337,40 +335,29 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * on the objective (the gradient pass, hi + lo always, sets the fixed point;
  * profiles/r04/accuracy); short runs follow slightly different trajectories.
  * bpgl_panel_mtm / _mm always use hi + lo operands.  bpgl_panel_get_tuning reads
- * "interleave1", "interleave2", "d_split", "lo8", "r_refresh", "carry_g", "g_refresh".
- * "lo8" (mask; a reset must follow): the lo piece of the residual (bit 0, pass 1)
- * and of the direction (bit 1, pass 2) on block-scaled e4m3 MFMA
- * (v_mfma_scale_f32_16x16x128_f8f6f4, twice the bf16 rate) against an e4m3 image of
- * A, the hi piece on bf16 as before: operands to ~2^-13 instead of ~2^-17.  Opt-in,
- * measured slower (the bf16 -> e4m3 conversions of the fragments cost more issue
- * time than the matrix cores save) and, in pass 1, less accurate (x within 3.4e-4
- * of the oracle instead of 2e-5).  With bit 1 the product S no longer equals A D'
- * exactly, so the incrementally updated residual is recomputed exactly (R = A X - B
- * from X's three bf16 pieces) every "r_refresh" iterations (default 128; 0 = never;
- * a multiple of 8).  lo8 passes use the interleave 0 / 1 / 2 mainloops with 8 waves.
+ * "interleave1", "interleave2", "d_split", "defer_x", "carry_g", "g_refresh".
+ * "defer_x" (0 / 1; default 1, one feature block; a reset must follow a change): the
+ * update x += gamma D' of an iteration is applied by the next pass-1 epilogue (and at
+ * the end of every bpgl_panel_step), bitwise the same x.
  * "carry_g" (0 / 1; default 1, in effect with one feature block only -- set to 1
  * with more blocks is an error; a reset must follow a change): the gradient is
  * carried in fp32, G_t = G_{t-1} + gamma_{t-1} A^T S_{t-1} with S_{t-1} = A D'_{t-1}
  * the previous iteration's product (its bf16 image: one MFMA product in pass 1
  * instead of the residual's two), and recomputed exactly from R (hi + lo) every
- * "g_refresh" iterations (default 64, a multiple of 8) and after every residual
- * refresh -- the single-RHS path's carried gradient.  Measured at configs[4]: pass 1
+ * "g_refresh" iterations (default 64, a multiple of 8) -- the single-RHS path's
+ * carried gradient.  Measured at configs[4]: pass 1
  * 226 -> 196 us, and after 1000 iterations x within 4e-6 of the oracle instead of
  * 1.9e-5 (fp32 accumulation of small updates instead of re-reading R through its
- * 2^-17 pieces).  With it, lo8 bit 0 is not used (pass 1 multiplies V).
- * get_tuning("carry_g") reports the form in effect. */
+ * 2^-17 pieces).  get_tuning("carry_g") reports the form in effect. */
 int bpgl_panel_set_tuning(bpgl_panel* ctx, const char* key, int64_t value);
 int bpgl_panel_get_tuning(const bpgl_panel* ctx, const char* key, int64_t* value);
 int bpgl_panel_geometry(const bpgl_panel* ctx, int32_t* kchunks);
-/* Counters since the last reset: "refreshes" (exact residual refreshes run),
- * "iters_enqueued", "exact_gradients" (carried gradient: iterations whose pass 1
- * computed G = A^T R exactly -- every g_refresh-th and the first after a refresh). */
+/* Counters since the last reset: "iters_enqueued", "exact_gradients" (carried
+ * gradient: iterations whose pass 1 computed G = A^T R exactly -- every g_refresh-th). */
 int bpgl_panel_stat(const bpgl_panel* ctx, const char* key, int64_t* value);
 /* The solver's fp64 residual R = A X - B, [nrhs][m] in device memory (valid after
  * the stream has drained). */
 const double* bpgl_panel_residual(bpgl_panel* ctx);
-/* Recompute R exactly from X now (the lo8 refresh; any lo8 setting). */
-int bpgl_panel_refresh(bpgl_panel* ctx);
 
 #ifdef __cplusplus
 }

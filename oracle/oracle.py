@@ -41,7 +41,8 @@ def lib():
         L.oracle_mv.argtypes = [ctypes.c_int, _p, _i64, _i64, _i64, _i64, _i32, _p, _p, ctypes.c_int]
         L.oracle_run.argtypes = [ctypes.c_int, _p, _i64, _i64, _i64, _i32, _i32, _p, _f64, _i64,
                                  _p, _f64, _p, _p, _p, _p, ctypes.c_int]
-        for f in (L.oracle_diag_ata, L.oracle_mtv, L.oracle_mv, L.oracle_run):
+        L.oracle_gauss_instance.argtypes = [ctypes.c_uint64, _i64, _i64, _f64, _p, _p, _p, ctypes.c_int]
+        for f in (L.oracle_diag_ata, L.oracle_mtv, L.oracle_mv, L.oracle_run, L.oracle_gauss_instance):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -112,6 +113,21 @@ def run(A, b, mu, nblock, iter_max, P=1, order=None, err_bound=None, x0=None,
     if want_gamma:
         out["gamma"] = gam
     return out
+
+
+def gauss_instance(seed, m, n, den=0.4, nthreads=0, A_out=None):
+    """The Gaussian-recipe instance of oracle/gauss_instance.c (parameters.py:17-33 with the
+    Irwin-Hall N(0, 1) approximant; bit-identical on every x86 host): (A fp32 [m][n], b, mu, x_true).
+    b = A x_true + e and mu = 0.1 ||A^T b||_inf with the oracle's thread-count-invariant products.
+    A_out: a C-contiguous float32 (m, n) array to fill (e.g. one view of pinned memory)."""
+    A = np.empty((m, n), dtype=np.float32) if A_out is None else A_out
+    assert A.dtype == np.float32 and A.shape == (m, n) and A.flags.c_contiguous
+    xt, e = np.zeros(n), np.zeros(m)
+    rc = lib().oracle_gauss_instance(int(seed), m, n, float(den), _ptr(A), _ptr(xt), _ptr(e), nthreads)
+    assert rc == 0, rc
+    b = mv(A, 0, n, xt, nthreads=nthreads) + e
+    mu = 0.1 * float(np.abs(mtv(A, 0, n, b, nthreads=nthreads)).max())
+    return A, b, mu, xt
 
 
 # ---------------------------------------------------------------------------

@@ -154,12 +154,10 @@ def test_drivers_on_device(golden, case):
         assert rel(drv.x, x) <= 1e-9
 
 
-@pytest.mark.parametrize("fused", [1, 0])
-def test_graph_and_eager_identical_and_deterministic(golden, fused):
+def test_graph_and_eager_identical_and_deterministic(golden):
     fx = golden("c1_b2_p4_f32in")
     A = oracle.fixture_A(fx)
     gc = make_cls("float")(A, 2, device=0)
-    gc.set_tuning("fused", fused)
     a = gc.run(fx["b"], float(fx["mu"]), 120, use_graph=True)["x"]
     b = gc.run(fx["b"], float(fx["mu"]), 120, use_graph=False)["x"]
     c = gc.run(fx["b"], float(fx["mu"]), 120, use_graph=True)["x"]
@@ -229,9 +227,8 @@ def test_objective_monotone_at_full_size():
 # column-sharded multi-rank kernels, with the all-reduce done by the test
 # (RCCL refuses two ranks on one GPU; the RCCL leg differs only by the call)
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("case,world", [("c1_b2_p4_f32in", 2), ("c1_b1_p1_f32in", 4), ("ragged_b3_p2_f32in", 2)])
-def test_external_exchange_ranks_match_single(golden, case, world, fused):
+def test_external_exchange_ranks_match_single(golden, case, world):
     from convex_optimization_amd import distributed as D
     fx = golden(case)
     A = oracle.fixture_A(fx)
@@ -239,7 +236,6 @@ def test_external_exchange_ranks_match_single(golden, case, world, fused):
     ranks = []
     for g in range(world):
         gc = make_cls("float")(D.shard_columns(A, B, g, world), B, device=0)
-        gc.set_tuning("fused", fused)
         gc.set_ranks(g, world)
         gc.solver_reset(fx["b"], float(fx["mu"]), record_len=IT, use_graph=False)
         ranks.append(gc)
@@ -261,9 +257,8 @@ def test_external_exchange_ranks_match_single(golden, case, world, fused):
     np.testing.assert_allclose(errs[0][:IT], fx["err_iter"][:IT], rtol=1e-6, atol=1e-9)
 
 
-@pytest.mark.parametrize("fused", [0, 1])
 @pytest.mark.parametrize("case", ["c1_b2_p4_f32in", "bound_b4_p2_f32in", "ragged_b3_p2_f32in"])
-def test_single_rank_rccl_path(golden, case, fused):
+def test_single_rank_rccl_path(golden, case):
     """The RCCL leg (comm init, all-reduce captured in the graph, k_step) with one rank on one GPU:
     same answers as the reference run and as the communicator-free solver."""
     from convex_optimization_amd import distributed as D
@@ -272,10 +267,8 @@ def test_single_rank_rccl_path(golden, case, fused):
     B, IT = int(fx["BLOCK"]), int(fx["ITER_MAX"])
     eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
     plain = make_cls("float")(A, B, device=0)
-    plain.set_tuning("fused", fused)
     ref = plain.run(fx["b"], float(fx["mu"]), IT, err_bound=eb, record=True)
     gc = make_cls("float")(A, B, device=0, comm=D.RankComm(0, 1))
-    gc.set_tuning("fused", fused)
     for graph in (True, False):
         res = gc.run(fx["b"], float(fx["mu"]), IT, err_bound=eb, record=True, use_graph=graph)
         assert res["t_last"] == int(fx["t_last"]) and res["stopped"] == bool(fx["stopped"])
@@ -298,33 +291,15 @@ def test_vendor_yardstick_reproduces_reference(golden, case):
     assert rel(v.solution(), fx["x"].reshape(-1)) <= 1e-9
 
 
-@pytest.mark.parametrize("fused", [1, 0])
-def test_tuning_knobs_do_not_change_results(golden, fused):
+def test_tuning_knobs_do_not_change_results(golden):
     fx = golden("c1_b2_p4_f32in")
     A = oracle.fixture_A(fx)
     gc = make_cls("float")(A, 2, device=0)
-    gc.set_tuning("fused", fused)
     base = gc.run(fx["b"], float(fx["mu"]), 50)["x"]
     for key, val in [("nt_loads", 0), ("tail_permille", 0), ("reverse_rows", 1), ("tail_permille", 1000),
                      ("nt_loads", 1), ("col_mode", 1), ("col_mode", 2), ("col_mode", 0)]:
         gc.set_tuning(key, val)
         np.testing.assert_array_equal(gc.run(fx["b"], float(fx["mu"]), 50)["x"], base)
-
-
-@pytest.mark.parametrize("case", ["c1_b2_p4_f32in", "random_b4_p1_f32in", "bound_b4_p2_f32in", "ragged_b3_p2_f32in"])
-def test_fused_and_unfused_iterations_agree(golden, case):
-    """Two-launch fused iteration (deferred update, last-arriver epilogues) vs the
-    six-kernel sequence: same algorithm, different summation order only."""
-    fx = golden(case)
-    A = oracle.fixture_A(fx)
-    B, IT = int(fx["BLOCK"]), int(fx["ITER_MAX"])
-    order = fx["order"] if bool(fx["random_order"]) else None
-    eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
-    gc = make_cls("float")(A, B, device=0)
-    outs = []
-    for fused in (1, 0):
-        gc.set_tuning("fused", fused)
-        outs.append(gc.run(fx["b"], float(fx["mu"]), IT, err_bound=eb, order=order, record=True))
-    assert outs[0]["t_last"] == outs[1]["t_last"] == int(fx["t_last"])
-    assert rel(outs[0]["x"], outs[1]["x"]) <= 1e-12
-    np.testing.assert_allclose(outs[0]["err_iter"], outs[1]["err_iter"], rtol=1e-9, atol=1e-12)
+    for gone in ("fused", "onepass_fold", "onepass_variant"):   # removed in round 5
+        with pytest.raises(Exception):
+            gc.set_tuning(gone, 0)

@@ -312,29 +312,3 @@ def test_iterate_recovers_without_iters_done(golden):
     assert gc.solver_stat("fallbacks") == 1
     xr = x[:gc.MAT_WIDTH].cpu().numpy()
     assert rel(xr, fx["x"]) <= 1e-9, rel(xr, fx["x"])
-
-
-@pytest.mark.parametrize("use_graph", [True, False])
-def test_in_kernel_fold_option(golden, use_graph):
-    """tuning key "onepass_fold" = 1 (opt-in, measured slower): k_onepass sums the
-    row groups' U partials itself (write-through partials, a per-segment meeting point) and the tail
-    reads the folded U.  The same iteration with the groups summed in another order: the reference
-    fixture within 1e-9, within 1e-12 of the default (tail-fold) form on a random problem."""
-    fx = golden("c1_b1_p1_f32in")
-    A = oracle.fixture_A(fx)
-    gc = make_cls("float")(A, 1, device=0)
-    gc.set_tuning("onepass", 1)
-    gc.set_tuning("onepass_fold", 1)
-    res = gc.run(fx["b"], float(fx["mu"]), int(fx["ITER_MAX"]), use_graph=use_graph)
-    assert gc.solver_stat("onepass") == 1 and gc.solver_stat("fallbacks") == 0
-    assert rel(res["x"], fx["x"]) <= 1e-9, rel(res["x"], fx["x"])
-    rs = np.random.RandomState(44)
-    A2 = rs.randn(3000, 20000) / np.sqrt(20000)
-    b2 = A2 @ np.where(rs.rand(20000) < 0.3, rs.randn(20000), 0.0) + 0.01 * rs.randn(3000)
-    mu2 = 0.1 * float(np.abs(A2.T @ b2).max())
-    g2 = make_cls("float")(A2, 1, device=0)
-    x0 = g2.run(b2, mu2, 120, use_graph=use_graph)["x"]
-    g2.set_tuning("onepass_fold", 1)
-    x1 = g2.run(b2, mu2, 120, use_graph=use_graph)["x"]
-    assert g2.solver_stat("onepass") == 1 and g2.solver_stat("fallbacks") == 0
-    assert rel(x1, x0) <= 1e-12, rel(x1, x0)

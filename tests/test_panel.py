@@ -112,44 +112,18 @@ def test_panel_interleave_knob_is_bitwise_neutral(k, d_split):
     pl = PanelLasso(Ab, 2, nrhs=k, device=0)
     pl.set_tuning("d_split", d_split)
     out = []
-    for v in (0, 1, 2, 3):            # 3: the staggered four-phase form (k = 128; others fall back to 2)
+    for v in (0, 1, 2):
         pl.set_tuning("interleave", v)
         out.append(pl.run(B, mu, 12)["x"])
     for o in out[1:]:
         np.testing.assert_array_equal(out[0], o)
-    for w in (0, 4) if k >= 64 else (0,):   # 16 waves per block
-        pl.set_tuning("interleave", 1)
-        pl.set_tuning("waves", w)
-        np.testing.assert_array_equal(pl.run(B, mu, 12)["x"], out[0])
-    pl.set_tuning("waves", 0)
     with pytest.raises(Exception):
-        pl.set_tuning("no_such_knob", 1)
+        pl.set_tuning("interleave", 3)     # the staggered form was removed in round 5
+    for gone in ("waves", "lo8", "write_through", "op_pad", "r_refresh", "no_such_knob"):
+        with pytest.raises(Exception):
+            pl.set_tuning(gone, 0)
     with pytest.raises(Exception):
         pl.set_tuning("d_split", 3)
-
-
-@pytest.mark.parametrize("blocks,d_split", [(1, 2), (2, 2), (2, 1)])
-def test_panel_padded_layouts_are_bitwise_neutral(blocks, d_split):
-    """op_pad (row pitch of the residual / direction images) and lda_pad (row pitch of the stored A)
-    change addresses only: solver iterates, products and the API GEMMs are bitwise identical."""
-    Ab, B, mu = instance(512, 2048, 64, seed=21)
-    ref = PanelLasso(Ab, blocks, nrhs=64, device=0)
-    ref.set_tuning("d_split", d_split)
-    x0 = ref.run(B, mu, 14)["x"]
-    R = np.random.RandomState(2).randn(512, 64)
-    D = np.random.RandomState(3).randn(2048 // blocks, 64)
-    G0, S0 = ref.mat_tMulMat(R, blocks - 1).cpu().numpy(), ref.matMulMat(D, 0).cpu().numpy()
-    for op_pad, lda_pad in ((64, 0), (0, 64), (192, 8)):
-        pl = PanelLasso(Ab, blocks, nrhs=64, device=0, op_pad=op_pad, lda_pad=lda_pad)
-        assert pl.get_tuning("op_pad") == op_pad
-        pl.set_tuning("d_split", d_split)
-        np.testing.assert_array_equal(pl.run(B, mu, 14)["x"], x0)
-        np.testing.assert_array_equal(pl.mat_tMulMat(R, blocks - 1).cpu().numpy(), G0)
-        np.testing.assert_array_equal(pl.matMulMat(D, 0).cpu().numpy(), S0)
-        with pytest.raises(Exception):
-            pl.set_tuning("op_pad", 0)     # layout knob: only before bind
-    with pytest.raises(Exception):
-        PanelLasso(Ab, blocks, nrhs=64, device=0, op_pad=32)   # not a multiple of 64
 
 
 @pytest.mark.parametrize("kchunks", [1, 2, 4, 16])
@@ -274,105 +248,21 @@ def _residual_drift(pl, Ab, B):
     return np.abs(R - Rex).max() / np.abs(Rex).max()
 
 
-@pytest.mark.parametrize("lo8,rr", [(1, 0), (2, 16), (3, 16), (3, 0)])
-@pytest.mark.parametrize("m,n,blocks,k,iters", [(512, 2048, 1, 32, 150), (512, 1024, 1, 128, 60),
-                                                (256, 1024, 2, 64, 80)])
-def test_panel_lo8_solver_matches_per_rhs_oracle(m, n, blocks, k, iters, lo8, rr):
-    """The e4m3 lo products (lo8 bit 0: the residual's lo piece in pass 1; bit 1: the direction's in
-    pass 2, with the exact residual refresh every rr iterations) meet the path's stated tolerance
-    against the per-RHS fp64 oracle on the same bf16 A: x within 1e-2 relative l2, objective within
-    1e-5 relative."""
-    Ab, B, mu = instance(m, n, k, seed=7 + k)
-    pl = PanelLasso(Ab, blocks, nrhs=k, device=0)
-    pl.set_tuning("d_split", 2)   # lo8 bit 1 replaces the direction's lo piece: the hi + lo form
-    pl.set_tuning("carry_g", 0)   # the carried gradient replaces pass 1's residual product
-    pl.set_tuning("lo8", lo8)
-    pl.set_tuning("r_refresh", rr)
-    assert (pl.get_tuning("lo8"), pl.get_tuning("r_refresh")) == (lo8, rr)
-    res = pl.run(B, mu, iters, record=True)
-    assert res["iters"] == iters
-    assert pl.stat("refreshes") == ((iters - 1) // rr if rr and lo8 & 2 else 0)
-    X = res["x"]
-    worst_x, worst_f = 0.0, 0.0
-    for j in range(0, k, max(1, k // 8)):
-        ref = oracle.run(Ab, B[:, j], mu[j], blocks, iters, nthreads=NT)["x"]
-        worst_x = max(worst_x, np.linalg.norm(X[:, j] - ref) / np.linalg.norm(ref))
-        f_dev, f_ref = objective(Ab, B[:, j], mu[j], X[:, j]), objective(Ab, B[:, j], mu[j], ref)
-        worst_f = max(worst_f, abs(f_dev - f_ref) / f_ref)
-    print(f"panel lo8={lo8} r_refresh={rr} m={m} n={n} k={k}: worst rel x {worst_x:.2e}, objective {worst_f:.2e}")
-    assert worst_x <= 1e-2
-    assert worst_f <= 1e-5
-    assert np.all(np.isfinite(res["err_iter"]))
-
-
 @pytest.mark.parametrize("carry", [0, 1])
-def test_panel_lo8_graph_equals_eager(carry):
-    """Graph replay and eager launches run the same lo8 kernels and the same refresh schedule (the
-    refresh runs between replays; with the carried gradient the iteration after a refresh computes G
-    exactly): bitwise equal iterates."""
-    Ab, B, mu = instance(512, 1024, 128, seed=4)
-    pl = PanelLasso(Ab, 1, nrhs=128, device=0)
-    pl.set_tuning("d_split", 2)
-    pl.set_tuning("carry_g", carry)
-    pl.set_tuning("lo8", 3 if not carry else 2)
-    pl.set_tuning("r_refresh", 16)
-    a = pl.run(B, mu, 44, use_graph=True)["x"]
-    assert pl.stat("refreshes") == 2
-    # with the carried gradient (g_refresh 64): iteration 0, and the first after each refresh (16, 32)
-    assert pl.stat("exact_gradients") == (3 if carry else 0)
-    b = pl.run(B, mu, 44, use_graph=False)["x"]
-    np.testing.assert_array_equal(a, b)
-    pl.solver_reset(B, mu)                      # split step calls: the schedule follows the iteration count
-    for n_it in (5, 3, 16, 9, 11):
-        pl.solver_step(n_it)
-    np.testing.assert_array_equal(pl.solver_x(), a)
-
-
-def test_panel_lo8_residual_refresh_pins_the_drift():
-    """lo8 in pass 2 makes the product S = A_hi D_hi + A8 D_lo8 differ from A D' (the direction the
-    update applies) by the e4m3 lo term's rounding, so the incrementally updated residual drifts
-    from A X - B; the refresh recomputes it from X's three exact bf16 pieces.  Measured here: the
-    drift without refreshes after 60 iterations is above the bf16 form's (fp32 accumulation only)
-    and below 1e-3 of max |R|; right after a refresh it is back below 1e-6 (fp32 accumulation over
-    a column chunk)."""
+def test_panel_residual_tracks_ax_minus_b(carry):
+    """The solver keeps R incrementally (R += gamma S, S = A D' from the MFMA pass) while x is stored
+    in fp32 (x += gamma D' rounded once per step); after 60 iterations R is within 1e-3 of max |R|
+    of A X - B recomputed in fp64 on the host, on both gradient forms, and the solve continues."""
     Ab, B, mu = instance(512, 2048, 64, seed=17)
     pl = PanelLasso(Ab, 1, nrhs=64, device=0)
-    pl.set_tuning("d_split", 2)
-    pl.set_tuning("carry_g", 0)
+    pl.set_tuning("carry_g", carry)
     pl.solver_reset(B, mu)
     pl.solver_step(60)
-    d_bf16 = _residual_drift(pl, Ab, B)
-    pl.set_tuning("lo8", 2)
-    pl.set_tuning("r_refresh", 0)
-    pl.solver_reset(B, mu)
-    pl.solver_step(60)
-    d_lo8 = _residual_drift(pl, Ab, B)
-    pl.refresh()
-    d_after = _residual_drift(pl, Ab, B)
-    print(f"residual drift after 60 iterations: bf16 {d_bf16:.2e}, lo8 {d_lo8:.2e}, lo8 after refresh {d_after:.2e}")
-    assert d_lo8 <= 1e-3
-    assert d_after <= 1e-6
-    assert d_after < d_lo8
-    pl.solver_step(20)                        # the solve continues from the refreshed residual
+    d = _residual_drift(pl, Ab, B)
+    print(f"carry_g={carry}: residual drift after 60 iterations {d:.2e}")
+    assert d <= 1e-3
+    pl.solver_step(20)
     assert np.all(np.isfinite(pl.solver_x()))
-
-
-def test_panel_lo8_knob_errors():
-    Ab, B, mu = instance(256, 512, 16, seed=2)
-    pl = PanelLasso(Ab, 1, nrhs=16, device=0, kchunks=8)   # 64-column chunks: too narrow for lo8 in pass 2
-    with pytest.raises(Exception):
-        pl.set_tuning("lo8", 2)
-    pl.set_tuning("lo8", 1)
-    with pytest.raises(Exception):
-        pl.set_tuning("lo8", 4)
-    with pytest.raises(Exception):
-        pl.set_tuning("r_refresh", 12)       # not a multiple of the 8-iteration graph
-    pl.solver_reset(B, mu)
-    pl.solver_step(2)
-    pl.set_tuning("lo8", 0)
-    with pytest.raises(Exception):
-        pl.solver_step(1)                    # a lo8 change needs a reset
-    assert PanelLasso(Ab, 1, nrhs=16, device=0).kchunks == 4   # the automatic chunks fit lo8 (128 | w / kchunks)
 
 
 @pytest.mark.parametrize("gp", [16, 64])
@@ -436,18 +326,14 @@ def test_panel_carried_gradient_graph_equals_eager():
 
 @pytest.mark.parametrize("k", [64, 128])
 def test_panel_carried_gradient_knobs_are_bitwise_neutral(k):
-    """One feature block with the carried gradient (the default): the interleave forms, 16-wave
-    blocks and the deferred-x placement's speed knobs change nothing in the iterates."""
+    """One feature block with the carried gradient (the default): the interleave forms change
+    nothing in the iterates."""
     Ab, B, mu = instance(512, 1024, k, seed=12)
     pl = PanelLasso(Ab, 1, nrhs=k, device=0)
     assert pl.get_tuning("carry_g") == 1
     out = []
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2):
         pl.set_tuning("interleave", v)
-        out.append(pl.run(B, mu, 20)["x"])
-    for w in (0, 4):
-        pl.set_tuning("interleave", 1)
-        pl.set_tuning("waves", w)
         out.append(pl.run(B, mu, 20)["x"])
     for o in out[1:]:
         np.testing.assert_array_equal(out[0], o)

@@ -44,16 +44,15 @@ def _exchange(ranks, fp32=False):
     torch.cuda.synchronize()
 
 
-def run_external(A, b, mu, world, iters, type_name="float", err_bound=None, refresh=64, fp32=False, fold=0):
+def run_external(A, b, mu, world, iters, type_name="float", err_bound=None, refresh=64, fp32=False):
     """`world` row-shard ranks on one GPU, the all-reduce done here (``fp32``: the fp32 wire
-    format of phases 0/1, summed in fp32 like RCCL; ``fold``: the "onepass_fold" knob)."""
+    format of phases 0/1, summed in fp32 like RCCL)."""
     ranks = []
     for g in range(world):
         gc = make_cls(type_name)(D.shard_rows(A, g, world), 1, device=0, shard="rows")
         gc.set_ranks(g, world)
         gc.set_tuning("onepass_refresh", refresh)
         gc.set_tuning("exchange_fp32", 1 if fp32 else 0)
-        gc.set_tuning("onepass_fold", fold)
         ranks.append(gc)
     diag = sum(gc._diag.clone() for gc in ranks)   # column norms: sums over ranks
     for g, gc in enumerate(ranks):
@@ -353,43 +352,3 @@ def test_two_pass_row_iteration_matches_plain_solver():
         assert rel(g1["x"], ref["x"]) <= 1e-10, rel(g1["x"], ref["x"])
         T = ref["t_last"] + 1
         np.testing.assert_allclose(g1["err_iter"][:T], ref["err_iter"][:T], rtol=1e-8, atol=1e-12)
-
-
-@pytest.mark.parametrize("fp32", [False, True])
-def test_in_kernel_fold_rows_is_bitwise(fp32):
-    """row shards with "onepass_fold" = 1: k_onepass writes the exchange buffer itself (the column
-    sums in the same group order as k_onepass_fold, the scalars by the last block to arrive) -- the
-    same bits as the separate fold kernel, with a one-rank RCCL communicator (the two caller-exchange
-    ranks: test_in_kernel_fold_external_ranks_is_bitwise)"""
-    rs = np.random.RandomState(9)
-    m, n = 1500, 12000
-    A = rs.randn(m, n) / np.sqrt(n)
-    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
-    mu = 0.1 * float(np.abs(A.T @ b).max())
-    rows = make_cls("float")(A, 1, device=0, comm=D.RankComm(0, 1), shard="rows")
-    rows.set_tuning("exchange_fp32", -1 if fp32 else 0)
-    ref = rows.run(b, mu, 120)["x"]
-    rows.set_tuning("onepass_fold", 1)
-    got = rows.run(b, mu, 120)["x"]
-    assert rows.solver_stat("onepass") == 1 and rows.solver_stat("fallbacks") == 0
-    np.testing.assert_array_equal(got, ref)
-
-
-@pytest.mark.parametrize("fp32", [False, True])
-def test_in_kernel_fold_external_ranks_is_bitwise(fp32):
-    """two caller-exchange row ranks (k_onepass writes [U | r.s23 | s23.s23 | failed] of each rank into
-    its exchange buffer itself, no fold launch; the test sums the buffers): "onepass_fold" 1 and 0 give
-    the same bits on both ranks, fp64 and fp32 exchange"""
-    rs = np.random.RandomState(12)
-    m, n = 1600, 12000
-    A = rs.randn(m, n) / np.sqrt(n)
-    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
-    mu = 0.1 * float(np.abs(A.T @ b).max())
-    out = {}
-    for fold in (0, 1):
-        ranks = run_external(A, b, mu, 2, 40, fp32=fp32, fold=fold)
-        xs = [gc.solver_x() for gc in ranks]
-        np.testing.assert_array_equal(xs[0], xs[1])
-        assert all(gc.solver_stat("onepass") == 1 and gc.solver_stat("fallbacks") == 0 for gc in ranks)
-        out[fold] = xs[0]
-    np.testing.assert_array_equal(out[0], out[1])

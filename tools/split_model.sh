@@ -9,7 +9,7 @@ OUT=gpurun_out/split_model
 mkdir -p $OUT
 run() {   # name, bench args...
     local name=$1; shift
-    timeout -k 10 240 python3 bench.py --no-cpu --steps 256 --warmup 100 --windows 3 "$@" > $OUT/$name.json 2> $OUT/$name.err || return 1
+    timeout -k 10 240 python3 bench.py --no-cpu --no-side-legs --steps 256 --warmup 100 --windows 3 "$@" > $OUT/$name.json 2> $OUT/$name.err || return 1
 }
 run rows_m8192_n65536   --comm --shard rows --m 8192 --n-per-gpu 65536 &&
 run rows_m4096_n65536   --comm --shard rows --m 4096 --n-per-gpu 65536 &&
