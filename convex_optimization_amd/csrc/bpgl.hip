@@ -1272,7 +1272,7 @@ int bpgl_kernel_times(bpgl_ctx* c, double* avg_ms, int64_t* samples) {
 }  // extern "C"
 
 #if BPGL_STAMP
-// diagnostic builds only: copy the [3][2][16384] block stamps to host memory
+// diagnostic builds only: copy the [3][5][16384] block stamps to host memory
 extern "C" int bpgl_diag_stamps(void* host_out) {
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(bpgl::g_stamps), sizeof(bpgl::g_stamps)) == hipSuccess ? 0 : -1;
 }

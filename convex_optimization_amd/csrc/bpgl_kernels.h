@@ -212,7 +212,9 @@ __device__ __forceinline__ void colpass_span(const T* __restrict__ Ab, long long
 #define BPGL_STAMP 0
 #endif
 #if BPGL_STAMP
-__device__ unsigned long long g_stamps[3][2][16384];   // [colpass, rowpass, onepass][start, end][block]
+// [colpass, rowpass, onepass][0 start, 1 end (after a barrier), 2-4 wave-0 marks (k_onepass: first
+// row computed, last row's phase 1, kernel end)][block]
+__device__ unsigned long long g_stamps[3][5][16384];
 #define BPGL_STAMP_AT(kern, se)                                                                   \
     do {                                                                                          \
         if ((se) == 1) __syncthreads();                                                           \

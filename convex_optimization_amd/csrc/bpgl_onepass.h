@@ -292,6 +292,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
                 for (int e = 0; e < N; ++e) acc[(k * N + e) & 3] = fma(v[e], d[k][e], acc[(k * N + e) & 3]);
             }
             const double s = op_wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+#if BPGL_STAMP
+            if ((t == 0 || t == nrows - 1) && threadIdx.x == 0 && b < 16384)
+                g_stamps[2][t == 0 ? 2 : 3][b] = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(s != s);
+#endif
             if (lane == 0)
                 __hip_atomic_store(&part[t % kOpSlots][wave], op_stuff(s, (unsigned)t >> kOpSlotsLog),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -413,6 +417,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
 #pragma unroll
             for (int e = 0; e < N; ++e) dst[col[k] + e] = u[k][e];
     if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) op_linesearch(p, o.ngroups);   // block-uniform
+#if BPGL_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0 && b < 16384) g_stamps[2][4][b] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // Row shards: this rank's exchange contribution [sum_groups U (wp) | sum r.s23 | sum s23.s23 |

@@ -45,6 +45,24 @@ static double gi_uniform(uint64_t seed, uint64_t stream, uint64_t idx) {
     return (double)(h >> 11) * 0x1.0p-53;
 }
 
+/* row i of A (fp32, unit l2 norm) into row[0..n) */
+static void gi_row(uint64_t seed, int64_t i, int64_t n, float* row) {
+    double ss = 0.0;
+    for (int64_t j = 0; j < n; ++j) {
+        const double z = gi_normal(seed, 1, (uint64_t)(i * n + j));
+        ss += z * z;
+    }
+    const double nrm = sqrt(ss);
+    for (int64_t j = 0; j < n; ++j) row[j] = (float)(gi_normal(seed, 1, (uint64_t)(i * n + j)) / nrm);
+}
+
+/* rows row0 .. row0 + nrows - 1 of the instance's A (a [nrows][n] fp32 slice) */
+int oracle_gauss_rows(uint64_t seed, int64_t row0, int64_t nrows, int64_t n, float* out) {
+    if (row0 < 0 || nrows < 0 || n <= 0) return -1;
+    for (int64_t i = 0; i < nrows; ++i) gi_row(seed, row0 + i, n, out + i * n);
+    return 0;
+}
+
 /*
  * A [m][n] fp32 (rows N(0, 1), unit l2 norm, each row normalised in fp64 before the one rounding
  * to fp32), x_true [n] (density den, N(0, 1) values), e [m] (N(0, 1e-4)).  Any output may be NULL.
@@ -59,16 +77,7 @@ int oracle_gauss_instance(uint64_t seed, int64_t m, int64_t n, double den, float
 #endif
     if (A) {
 #pragma omp parallel for schedule(static)
-        for (int64_t i = 0; i < m; ++i) {
-            float* row = A + i * n;
-            double ss = 0.0;
-            for (int64_t j = 0; j < n; ++j) {
-                const double z = gi_normal(seed, 1, (uint64_t)(i * n + j));
-                ss += z * z;
-            }
-            const double nrm = sqrt(ss);
-            for (int64_t j = 0; j < n; ++j) row[j] = (float)(gi_normal(seed, 1, (uint64_t)(i * n + j)) / nrm);
-        }
+        for (int64_t i = 0; i < m; ++i) gi_row(seed, i, n, A + i * n);
     }
     if (x_true)
         for (int64_t j = 0; j < n; ++j)

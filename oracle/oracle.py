@@ -42,7 +42,9 @@ def lib():
         L.oracle_run.argtypes = [ctypes.c_int, _p, _i64, _i64, _i64, _i32, _i32, _p, _f64, _i64,
                                  _p, _f64, _p, _p, _p, _p, ctypes.c_int]
         L.oracle_gauss_instance.argtypes = [ctypes.c_uint64, _i64, _i64, _f64, _p, _p, _p, ctypes.c_int]
-        for f in (L.oracle_diag_ata, L.oracle_mtv, L.oracle_mv, L.oracle_run, L.oracle_gauss_instance):
+        L.oracle_gauss_rows.argtypes = [ctypes.c_uint64, _i64, _i64, _i64, _p]
+        for f in (L.oracle_diag_ata, L.oracle_mtv, L.oracle_mv, L.oracle_run, L.oracle_gauss_instance,
+                  L.oracle_gauss_rows):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -128,6 +130,13 @@ def gauss_instance(seed, m, n, den=0.4, nthreads=0, A_out=None):
     b = mv(A, 0, n, xt, nthreads=nthreads) + e
     mu = 0.1 * float(np.abs(mtv(A, 0, n, b, nthreads=nthreads)).max())
     return A, b, mu, xt
+
+
+def gauss_rows(seed, row0, nrows, n):
+    """rows row0 .. row0 + nrows - 1 of gauss_instance's A, without building the rest"""
+    out = np.empty((nrows, n), dtype=np.float32)
+    assert lib().oracle_gauss_rows(int(seed), int(row0), int(nrows), int(n), _ptr(out)) == 0
+    return out
 
 
 # ---------------------------------------------------------------------------

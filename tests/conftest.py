@@ -20,7 +20,7 @@ def pytest_configure(config):
 
 def golden_cases():
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and f != "kats.npz" and not f.startswith("longrun_"))
+                  if f.endswith(".npz") and f != "kats.npz" and not f.startswith(("longrun_", "gauss_")))
 
 
 @pytest.fixture(scope="session")

@@ -117,3 +117,31 @@ def test_dropin_run_of_reference_driver_is_bitwise():
         assert sorted(a.files) == sorted(b.files)
         for k in b.files:
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"{name}:{k}")
+
+
+def test_gauss_instance_is_deterministic_and_gaussian():
+    """oracle/gauss_instance.c (the Gaussian-recipe instance of the full-size fixture): the same bits
+    for any thread count and from the row-slice generator, rows of unit l2 norm, N(0, 1)-like
+    entries (Irwin-Hall: mean 0, kurtosis 2.9 against 3), density 0.4 of x_true"""
+    A1, b1, mu1, x1 = oracle.gauss_instance(7, 512, 1024, nthreads=1)
+    A2, b2, mu2, x2 = oracle.gauss_instance(7, 512, 1024, nthreads=5)
+    assert np.array_equal(A1, A2) and np.array_equal(b1, b2) and mu1 == mu2 and np.array_equal(x1, x2)
+    assert np.array_equal(oracle.gauss_rows(7, 100, 3, 1024), A1[100:103])
+    np.testing.assert_allclose(np.linalg.norm(A1.astype(np.float64), axis=1), 1.0, rtol=1e-6)
+    z = A1.astype(np.float64).reshape(-1) * np.sqrt(1024)
+    assert abs(z.mean()) < 0.01 and abs(z.var() - 1) < 0.01
+    assert 2.8 < ((z - z.mean()) ** 4).mean() / z.var() ** 2 < 3.0
+    assert abs((x1 != 0).mean() - 0.4) < 0.05
+    assert not np.array_equal(A1, oracle.gauss_instance(8, 512, 1024)[0])
+
+
+def test_gauss_fixture_samples_match_the_generator():
+    """tests/golden/gauss_configs3.npz (configs[3] at full size, C oracle, tests/golden/make_gauss.py)
+    was made from this generator: its stored A samples of 64 rows are regenerated bit for bit"""
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "gauss_configs3.npz")
+    fx = dict(np.load(path))
+    n, seed = int(fx["n"]), int(fx["seed"])
+    for r, c, v in list(zip(fx["A_rows"], fx["A_cols"], fx["A_samples"]))[:64]:
+        assert oracle.gauss_rows(seed, int(r), 1, n)[0, int(c)] == v
+    assert fx["x"].shape == (n,) and int(fx["iters"]) >= 260 and np.isfinite(fx["objective"])
