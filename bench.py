@@ -160,6 +160,11 @@ def parse():
                          "hi+lo gradients (1); -1: library default")
     ap.add_argument("--g-refresh", type=int, default=-1,
                     help="panel path with carry_g: exact gradient period (multiple of 8); -1: library default")
+    ap.add_argument("--fuse-update", type=int, default=-1, choices=[-1, 0, 1],
+                    help="panel path, one block with x deferred: reduce + line search + residual update in one "
+                         "launch (1) or two (0); -1: library default")
+    ap.add_argument("--fuse-grid", type=int, default=-1, choices=[-1, 256, 512, 1024],
+                    help="panel path: blocks of the fused reduce + update launch (-1: library default)")
     ap.add_argument("--defer-x", type=int, default=-1, choices=[-1, 0, 1],
                     help="panel path, one block: apply x += gamma D in the next pass-1 epilogue (1) or in the "
                          "update kernel (0); -1: library default")
@@ -666,6 +671,10 @@ def measure_panel(args):
         pl.set_tuning("d_split", args.d_split)
     if args.defer_x >= 0:
         pl.set_tuning("defer_x", args.defer_x)
+    if args.fuse_update >= 0:
+        pl.set_tuning("fuse_update", args.fuse_update)
+    if args.fuse_grid > 0:
+        pl.set_tuning("fuse_grid", args.fuse_grid)
     if args.carry_g >= 0:
         pl.set_tuning("carry_g", args.carry_g)
     if args.g_refresh >= 0:
@@ -724,6 +733,7 @@ def measure_panel(args):
             "m": m, "n": n, "nrhs": k, "feature_blocks": args.block, "kchunks": pl.kchunks,
             "interleave": args.interleave, "d_split": d_split, "defer_x": pl.get_tuning("defer_x"),
             "carry_g": carry, "g_refresh": g_period, "exact_gradients": pl.stat("exact_gradients"),
+            "fuse_update": pl.get_tuning("fuse_update"), "fuse_grid": pl.get_tuning("fuse_grid"),
             "interleave12": [pl.get_tuning("interleave1"), pl.get_tuning("interleave2")],
             "alg_bytes_per_iter": alg_iter,
             "hbm_roofline_iters_per_s": HBM_PEAK_GBS * 1e9 / alg_iter,
@@ -848,7 +858,8 @@ def panel_leg(args):
             "rhs_iters_per_s": c["rhs_iters_per_s"], "iter_roofline_frac": c["iter_roofline_frac"],
             "hbm_roofline_iters_per_s": c["hbm_roofline_iters_per_s"], "windows_s": c["windows_s"],
             "kernel_avg_ms": c["kernel_avg_ms"], "status": c["status"],
-            "tuning": {q: c[q] for q in ("d_split", "carry_g", "g_refresh", "defer_x", "kchunks", "interleave12")},
+            "tuning": {q: c[q] for q in ("d_split", "carry_g", "g_refresh", "defer_x", "fuse_update", "kchunks",
+                                         "interleave12")},
             "roofline": p["roofline"]}
 
 
@@ -983,6 +994,12 @@ def main():
         "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": scaling,
+        # rounds 1-3 keyed the N > 1 value on the weak problem (block-iters/s); since round 4
+        # it is the strong form (iters/s of the 8192 x 65536 matrix) unless --weak -- compare only lines
+        # with the same "scaling"
+        "value_semantics": {"none": "iters/s of the configured matrix on one GPU",
+                            "strong": "iters/s of the fixed matrix split over the N GPUs (rounds >= 4)",
+                            "weak": "block-iters/s = N x iters/s of m x 65536 N (the rounds 1-3 N > 1 value)"}[scaling],
         "vs_baseline": None,
         "dtype": "f64",
         "a_dtype": {"float": "fp32", "double": "fp64", "bf16": "bf16"}[args.type],

@@ -68,7 +68,8 @@ struct PanelState {
     double last_err;
     long long cur_mb;   // block of the iteration being finished (set by the line search)
     long long pending;  // one feature block: x += gamma D' of the last iteration not yet applied
-    long long pad[3];
+    long long fail;     // k_panel_reduce_upd: a block waited for its RHS's step size in vain (not co-resident)
+    long long pad[2];
 };
 
 struct PanelParams {
@@ -103,6 +104,9 @@ struct PanelParams {
     float* Gc;          // [k][w]   the carried gradient (fp32)
     __bf16* Sh;         // [k][ldr] pass 1's operand in a carried iteration: bf16(V), V = gamma S + E (k_panel_update)
     float* Ec;          // [k][m]   V - bf16(V): the rounding error fed into the next carried operand
+    // k_panel_reduce_upd (the reduce, line search and residual update in one launch)
+    unsigned long long* ready;   // [k] per RHS: the arrival count at which its step size was published
+    unsigned long long* lsdone;  // line searches finished (monotone, + k per launch): the last one bumps t
 };
 
 constexpr int kLspRows = 1024;    // rows per line-search partial
@@ -994,8 +998,9 @@ __device__ void panel_step_rhs(const PanelParams& p, int rhs, double a, double b
         e = s3[2][0];
         for (int q = 1; q < kWaves; ++q) e = (s3[2][q] > e || s3[2][q] != s3[2][q]) ? s3[2][q] : e;
         const double r1 = rs + p.mu[rhs] * (a - b);
-        p.gamma[rhs] = (ss == 0.0) ? 0.0 : proj(-r1 / ss, 0.0, 1.0);
-        p.err_rhs[rhs] = e;
+        // write-through: k_panel_reduce_upd's other blocks read them in the same launch
+        panel_st_sc1(p.gamma + rhs, (ss == 0.0) ? 0.0 : proj(-r1 / ss, 0.0, 1.0));
+        panel_st_sc1(p.err_rhs + rhs, e);
         if (rhs == 0) p.st->cur_mb = p.st->t % p.nblock;   // nobody else reads it in this launch
     }
 }
@@ -1158,6 +1163,161 @@ __global__ __launch_bounds__(kThreads) void k_panel_update1(PanelParams p, int c
     if (blockIdx.x == 0 && threadIdx.x < 64) panel_bump_t(p, true);
 }
 
+// One feature block with x deferred (the default configs[4] iteration): k_panel_reduce (S = the
+// fixed-order sum of the chunk slabs, the line-search partials, each RHS's last block running its
+// line search) and k_panel_update1 (R += gamma S, the carried operand, R's images) in ONE launch.
+// Grid = k x G, G blocks per RHS, block g of RHS j owning its U 1024-row groups; a thread owns 4
+// rows per group and keeps their S, R (and E) in registers across the line search: the blocks of an
+// RHS that are not last wait (bounded, one lane polling an sc1 word) for the step size its last block
+// publishes, then update their own rows -- S is never stored and R, S, E are read once (the two
+// kernels read R twice and wrote and re-read S).  Every sum is the two kernels' (per 1024-row group:
+// the 4 rows of a lane, wave sums, the 4 waves in order; the groups in order), so the iterates are
+// bitwise those of the two-kernel path.  Needs the k x G blocks co-resident (k x G <= the occupancy x
+// CUs, checked at bind, where the library picks this form; nothing else runs on the stream between);
+// a wait that runs out sets PanelState::fail, updates nothing, and bpgl_panel_status reports it.
+// The last line search to finish (lsdone) ends the iteration as k_panel_update1 does (t + 1, the
+// error record, x pending).
+constexpr unsigned kPanelPolls = 1u << 20;
+template <int U>
+__global__ __launch_bounds__(kThreads) void k_panel_reduce_upd(PanelParams p, int cflag, int G) {
+    const int rhs = blockIdx.x % p.k;
+    const int g = blockIdx.x / p.k;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double na = 0.0, nb = 0.0, ne = 0.0;
+    panel_norm_share(p, rhs, na, nb, ne);
+    const long long cstride = (long long)p.k * p.m;
+    double s[U][4], r[U][4];
+    float4 ev[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const long long e = (long long)rhs * p.m + (long long)(g * U + u) * kLspRows + 4 * threadIdx.x;
+        const double2 r01 = *reinterpret_cast<const double2*>(p.R + e);
+        const double2 r23 = *reinterpret_cast<const double2*>(p.R + e + 2);
+        r[u][0] = r01.x; r[u][1] = r01.y; r[u][2] = r23.x; r[u][3] = r23.y;
+        ev[u] = (cflag & 3) == 1 ? *reinterpret_cast<const float4*>(p.Ec + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float* src = p.Sslab + e;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[u][q] = 0.0;
+        int c = 0;
+        for (; c + 8 <= p.kchunks; c += 8) {   // 8 loads in flight, the adds in chunk order
+            float4 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(src + (c + q) * cstride);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                s[u][0] += (double)v[q].x; s[u][1] += (double)v[q].y; s[u][2] += (double)v[q].z; s[u][3] += (double)v[q].w;
+            }
+        }
+        for (; c < p.kchunks; ++c) {
+            const float4 v = *reinterpret_cast<const float4*>(src + c * cstride);
+            s[u][0] += (double)v.x; s[u][1] += (double)v.y; s[u][2] += (double)v.z; s[u][3] += (double)v.w;
+        }
+    }
+    // per-group line-search partials, in k_panel_reduce's order
+    __shared__ double sr[U][kWaves], sq[U][kWaves];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        double rs = 0.0, ss = 0.0;
+        rs = fma(r[u][0], s[u][0], rs); rs = fma(r[u][1], s[u][1], rs);
+        rs = fma(r[u][2], s[u][2], rs); rs = fma(r[u][3], s[u][3], rs);
+        ss = fma(s[u][0], s[u][0], ss); ss = fma(s[u][1], s[u][1], ss);
+        ss = fma(s[u][2], s[u][2], ss); ss = fma(s[u][3], s[u][3], ss);
+        rs = wave_sum(rs);
+        ss = wave_sum(ss);
+        if (lane == 0) { sr[u][wave] = rs; sq[u][wave] = ss; }
+    }
+    __syncthreads();
+    __shared__ int last, ok;
+    __shared__ unsigned long long target;
+    __shared__ double gsh;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            double* dst = p.lsp + ((long long)(g * U + u) * p.k + rhs) * 2;
+            panel_st_sc1(dst, ((sr[u][0] + sr[u][1]) + sr[u][2]) + sr[u][3]);
+            panel_st_sc1(dst + 1, ((sq[u][0] + sq[u][1]) + sq[u][2]) + sq[u][3]);
+        }
+        // the sc1 hand-off of k_panel_reduce (no agent fences; see op_arrive_last)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long old = __hip_atomic_fetch_add(p.cnt + rhs, 1ull, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+        last = ((old + 1) % (unsigned long long)G) == 0;
+        target = (old / (unsigned long long)G + 1) * (unsigned long long)G;
+        ok = 1;
+    }
+    __syncthreads();
+    if (last) {
+        panel_step_rhs<true>(p, rhs, na, nb, ne);   // gamma, err_rhs (sc1)
+        if (threadIdx.x == 0) {
+            gsh = panel_ld_sc1(p.gamma + rhs);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(p.ready + rhs, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long d = __hip_atomic_fetch_add(p.lsdone, 1ull, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+            last = ((d + 1) % (unsigned long long)p.k) == 0 ? 2 : 1;   // 2: the last line search of the launch
+        }
+    } else if (threadIdx.x == 0) {
+        unsigned n = kPanelPolls;
+        while (__hip_atomic_load(p.ready + rhs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (n-- == 0) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (ok) gsh = panel_ld_sc1(p.gamma + rhs);
+        else __hip_atomic_store(reinterpret_cast<unsigned long long*>(&p.st->fail), 1ull, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!ok) return;   // block-uniform: nothing is updated (bpgl_panel_status reports the failure)
+    const double gm = gsh;
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const long long e = (long long)rhs * p.m + (long long)(g * U + u) * kLspRows + 4 * threadIdx.x;
+        const long long re = (long long)rhs * p.ldr + (e - (long long)rhs * p.m);
+        double rn[4];
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rn[q] = r[u][q] + gm * s[u][q];
+        if (cflag) {   // the carried operand V = E + gamma S (panel_put_carry, E preloaded)
+            const float e4[4] = {ev[u].x, ev[u].y, ev[u].z, ev[u].w};
+            __bf16 h[4];
+            float rr[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double v = (double)e4[q] + gm * s[u][q];
+                h[q] = to_bf16((float)v);
+                rr[q] = (float)(v - (double)(float)h[q]);
+            }
+            *reinterpret_cast<bf16x4v*>(p.Sh + re) = bf16x4v{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<float4*>(p.Ec + e) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+        }
+        put(p.R, e, make_double2(rn[0], rn[1]));
+        put(p.R, e + 2, make_double2(rn[2], rn[3]));
+        if (!(cflag & 4)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) split_bf16(rn[q], hi[q], lo[q]);
+            put(p.Rh, re, bf16x4v{hi[0], hi[1], hi[2], hi[3]});
+            put(p.Rl, re, bf16x4v{lo[0], lo[1], lo[2], lo[3]});
+        }
+    }
+    if (last == 2 && threadIdx.x < 64) {   // every RHS's err_rhs is published (sc1): end the iteration
+        double e = 0.0;
+        for (int j = threadIdx.x; j < p.k; j += 64) {
+            const double v = panel_ld_sc1(p.err_rhs + j);
+            e = (v > e || v != v) ? v : e;
+        }
+        e = wave_max(e);
+        if (threadIdx.x == 0) {
+            const long long t = p.st->t;
+            if (p.err_iter && t < p.rec_len) p.err_iter[t] = e;
+            p.st->last_err = e;
+            p.st->t = t + 1;
+            p.st->iters = t + 1;
+            p.st->pending = 1;
+        }
+    }
+}
+
 // apply a pending x += gamma D' (one feature block) -- the end of every bpgl_panel_step, so the
 // iterates the caller reads are current; a no-op when nothing is pending
 template <int DS>
@@ -1240,6 +1400,7 @@ __global__ void k_panel_reset_state(PanelParams p) {
         p.st->last_err = 0.0;
         p.st->cur_mb = 0;
         p.st->pending = 0;
+        p.st->fail = 0;
     }
 }
 

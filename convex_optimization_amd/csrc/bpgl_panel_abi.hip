@@ -39,6 +39,9 @@ struct bpgl_panel {
     int64_t g_period = 64;        // exact gradient every g_period iterations ("g_refresh" knob)
     int gm_cur = 0;               // pass-1 form of the launch being enqueued: 0 plain, 1 exact + store G, 2 carried
     hipGraphExec_t gexec_ref = nullptr;   // carry_g: a graph whose first iteration is the exact-gradient one
+    int fuse_update = 1;          // one block, x deferred: reduce + line search + R update in one launch ("fuse_update")
+    int fuse_ok = 0;              // ... and the shape and occupancy admit it (panel_fused_geo, set at bind)
+    int fuse_grid = 256;          // its grid: at most this many blocks, k x G ("fuse_grid": 256, 512 or 1024)
     int64_t t_host = 0;           // iterations enqueued since the last reset
     int64_t n_exact = 0;          // carried gradient: exact-gradient iterations since the last reset
     int64_t ldr() const { return m; }
@@ -48,7 +51,8 @@ struct bpgl_panel {
 namespace {
 
 struct PanelLayout {
-    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, Gc, Sh, Ec, total;
+    int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, ready, lsdone, Gc,
+        Sh, Ec, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -73,6 +77,8 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.gamma = k.take(8 * c->k);
     L.err_rhs = k.take(8 * c->k);
     L.cnt = k.take(8 * (int64_t)c->k);
+    L.ready = k.take(8 * (int64_t)c->k);
+    L.lsdone = k.take(8);
     // the carried gradient's state (one feature block only; ADVICE r04: not reserved otherwise)
     const bool carry = c->nblock == 1;
     L.Gc = k.take(carry ? 4 * kw : 0);                           // the carried gradient (fp32)
@@ -147,6 +153,44 @@ int panel_launch(bpgl_panel* c, int which, int fixed_block, double* out, int mod
 }
 bool panel_carry(const bpgl_panel* c) { return c->carry_g && c->nblock == 1; }
 int panel_pass(bpgl_panel* c, int which) { return panel_launch(c, which, -1, nullptr, 1, c->dsplit); }
+// k_panel_reduce_upd's geometry: G blocks per RHS of U 1024-row groups each (k x G <= fuse_grid
+// blocks); false when the shape does not admit it (m a multiple of 1024, U in {1, 2, 4})
+bool panel_fused_geo(const bpgl_panel* c, int* G, int* U) {
+    if (c->m % kLspRows) return false;
+    const int64_t groups = c->m / kLspRows;
+    const int64_t g = std::min<int64_t>(std::max<int64_t>(1, c->fuse_grid / c->k), groups);
+    if (groups % g) return false;
+    const int64_t u = groups / g;
+    if (u != 1 && u != 2 && u != 4) return false;
+    *G = (int)g;
+    *U = (int)u;
+    return true;
+}
+const void* panel_fused_fn(int U) {
+    return U == 1 ? (const void*)k_panel_reduce_upd<1> : U == 2 ? (const void*)k_panel_reduce_upd<2>
+                                                              : (const void*)k_panel_reduce_upd<4>;
+}
+int panel_reduce_upd(bpgl_panel* c, int cflag) {
+    int G = 0, U = 0;
+    (void)panel_fused_geo(c, &G, &U);
+    const dim3 grid((unsigned)(c->k * G)), blk(kThreads);
+    if (U == 1) hipLaunchKernelGGL(k_panel_reduce_upd<1>, grid, blk, 0, c->stream, c->p, cflag, G);
+    else if (U == 2) hipLaunchKernelGGL(k_panel_reduce_upd<2>, grid, blk, 0, c->stream, c->p, cflag, G);
+    else hipLaunchKernelGGL(k_panel_reduce_upd<4>, grid, blk, 0, c->stream, c->p, cflag, G);
+    LAUNCH_CHECK("k_panel_reduce_upd");
+    return 0;
+}
+// the fused reduce + update needs its k x G blocks resident together
+void panel_fuse_check(bpgl_panel* c) {
+    int G = 0, U = 0, nb = 0, cus = 0;
+    c->fuse_ok = 0;
+    if (panel_fused_geo(c, &G, &U) &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, panel_fused_fn(U), kThreads, 0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess &&
+        (int64_t)nb * cus >= (int64_t)c->k * G)
+        c->fuse_ok = 1;
+    (void)hipGetLastError();
+}
 int panel_reduce(bpgl_panel* c, double* out, int mode) {
     hipLaunchKernelGGL(k_panel_reduce, dim3((unsigned)(c->k * cdiv(c->m, kLspRows))), dim3(kThreads), 0, c->stream,
                        c->p, out, mode);
@@ -182,6 +226,11 @@ int panel_iteration(bpgl_panel* c, int64_t it, bool exact = false, bool split_r 
     if ((rc = panel_pass(c, 1))) return rc;
     panel_ev(c, it, 1, 1);
     panel_ev(c, it, 2, 0);
+    if (c->nblock == 1 && c->defer_x && c->fuse_update && c->fuse_ok) {   // reduce + line search + R update
+        rc = panel_reduce_upd(c, cflag);
+        panel_ev(c, it, 2, 1);
+        return rc;
+    }
     if ((rc = panel_reduce(c, c->p.S, 1))) return rc;   // its last block per RHS runs the line search
     panel_ev(c, it, 2, 1);
     panel_ev(c, it, 4, 0);
@@ -321,8 +370,11 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.cnt = (unsigned long long*)(s + L.cnt);
     p.Gc = (float*)(s + L.Gc);
     p.Ec = (float*)(s + L.Ec);
+    p.ready = (unsigned long long*)(s + L.ready);
+    p.lsdone = (unsigned long long*)(s + L.lsdone);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
+    panel_fuse_check(c);
     c->bound = true;
     c->have_diag = false;
     c->solver = false;
@@ -385,6 +437,8 @@ int bpgl_panel_reset(bpgl_panel* c, const double* B, const double* mu, double* e
     p.err_iter = err_iter;
     p.rec_len = err_iter ? record_len : 0;
     HIP_TRY(hipMemsetAsync(p.cnt, 0, 8 * (int64_t)c->k, c->stream));   // arrival counters start at 0
+    HIP_TRY(hipMemsetAsync(p.ready, 0, 8 * (int64_t)c->k, c->stream));
+    HIP_TRY(hipMemsetAsync(p.lsdone, 0, 8, c->stream));
     hipLaunchKernelGGL(k_panel_reset_state, dim3(1), dim3(64), 0, c->stream, c->p);
     LAUNCH_CHECK("k_panel_reset_state");
     p.Sh = panel_carry(c) ? (__bf16*)((char*)p.st + (panel_layout(c).Sh - panel_layout(c).st)) : nullptr;
@@ -463,6 +517,10 @@ int bpgl_panel_status(bpgl_panel* c, int64_t* iters, double* last_err) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (iters) *iters = st.iters;
     if (last_err) *last_err = st.last_err;
+    if (st.fail)
+        return fail(BPGL_E_EXCHANGE, "k_panel_reduce_upd: a block waited in vain for its right-hand side's step size "
+                                     "(blocks not co-resident: another kernel held CUs); the iterates are not valid -- "
+                                     "reset and run with the tuning key fuse_update = 0");
     return 0;
 }
 
@@ -502,6 +560,15 @@ int bpgl_panel_set_tuning(bpgl_panel* c, const char* key, int64_t value) {
         if (value < 0 || value > 2) return fail(BPGL_E_ARG, "interleave must be 0, 1 or 2");
         if (both || key[10] == '1') c->interleave[0] = (int)value;
         if (both || key[10] == '2') c->interleave[1] = (int)value;
+    } else if (!strcmp(key, "fuse_grid")) {
+        if (value != 256 && value != 512 && value != 1024) return fail(BPGL_E_ARG, "fuse_grid must be 256, 512 or 1024");
+        c->fuse_grid = (int)value;
+        panel_fuse_check(c);
+        c->solver = false;
+    } else if (!strcmp(key, "fuse_update")) {
+        if (value != 0 && value != 1) return fail(BPGL_E_ARG, "fuse_update must be 0 or 1");
+        c->fuse_update = (int)value;
+        c->solver = false;   // the graphs bake the launch sequence in: a reset must follow
     } else if (!strcmp(key, "defer_x")) {
         if (value != 0 && value != 1) return fail(BPGL_E_ARG, "defer_x must be 0 or 1");
         c->defer_x = (int)value;
@@ -532,6 +599,8 @@ int bpgl_panel_get_tuning(const bpgl_panel* c, const char* key, int64_t* value) 
     else if (!strcmp(key, "interleave2")) *value = panel_ilv(c, 1, c->dsplit);   // the solver's pass 2
     else if (!strcmp(key, "d_split")) *value = c->dsplit;
     else if (!strcmp(key, "defer_x")) *value = c->defer_x;
+    else if (!strcmp(key, "fuse_grid")) *value = c->fuse_grid;
+    else if (!strcmp(key, "fuse_update")) *value = c->nblock == 1 && c->defer_x && c->fuse_update && c->fuse_ok;   // in effect
     else if (!strcmp(key, "carry_g")) *value = panel_carry(c) ? 1 : 0;   // the form in effect
     else if (!strcmp(key, "g_refresh")) *value = c->g_period;
     else return fail(BPGL_E_ARG, "unknown panel tuning key '%s'", key);

@@ -358,3 +358,42 @@ def test_panel_carried_gradient_is_closer_to_the_oracle():
     print(f"200 iterations, worst rel x against the oracle: exact {err[0]:.2e}, carried {err[1]:.2e}")
     assert err[1] <= 1e-3
     assert err[1] <= 1.5 * err[0]
+
+
+@pytest.mark.parametrize("k,m", [(16, 1024), (32, 2048), (64, 2048), (128, 1024), (128, 4096)])
+def test_panel_fused_reduce_update_is_bitwise(k, m):
+    """k_panel_reduce_upd (one feature block, x deferred: the split-K reduce, each RHS's line search
+    and R += gamma S in one launch, the blocks of an RHS waiting for the step size its last block
+    publishes) sums in the two kernels' order: the iterates, the error record and the residual are
+    bitwise those of k_panel_reduce + k_panel_update1, graph and eager, across exact-gradient
+    iterations (g_refresh 16)"""
+    Ab, B, mu = instance(m, 1024, k, seed=23)
+    out = {}
+    for fuse in (1, 0):
+        pl = PanelLasso(Ab, 1, nrhs=k, device=0)
+        pl.set_tuning("fuse_update", fuse)
+        pl.set_tuning("g_refresh", 16)
+        assert pl.get_tuning("fuse_update") == fuse
+        res = pl.run(B, mu, 40, record=True)
+        assert res["iters"] == 40
+        r = pl.residual_device().cpu().numpy().copy()
+        eager = pl.run(B, mu, 40, record=True, use_graph=False)
+        np.testing.assert_array_equal(eager["x"], res["x"])
+        out[fuse] = (res["x"], res["err_iter"], r)
+    for a, b in zip(out[1], out[0]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_panel_fused_reduce_update_eligibility():
+    """the fused form needs m a multiple of 1024 (whole line-search groups) and one feature block with
+    x deferred; elsewhere the two kernels run (get_tuning reports the form in effect)"""
+    Ab, B, mu = instance(512, 1024, 32, seed=3)
+    assert PanelLasso(Ab, 1, nrhs=32, device=0).get_tuning("fuse_update") == 0    # m = 512
+    Ab, B, mu = instance(1024, 2048, 32, seed=3)
+    assert PanelLasso(Ab, 2, nrhs=32, device=0).get_tuning("fuse_update") == 0    # two feature blocks
+    pl = PanelLasso(Ab, 1, nrhs=32, device=0)
+    assert pl.get_tuning("fuse_update") == 1
+    pl.set_tuning("defer_x", 0)
+    assert pl.get_tuning("fuse_update") == 0
+    with pytest.raises(Exception):
+        pl.set_tuning("fuse_update", 2)
