@@ -196,7 +196,7 @@ int op_cache_eff(const bpgl_ctx* c) {
 
 // scratch layout (offsets in bytes)
 struct Layout {
-    int64_t slab_g, slab_s, g, D, parts, parts2, comm, r, Ax, st, diag, rec, opG, opUs, opPG, opS, opABE, total;
+    int64_t slab_g, slab_s, D, parts, parts2, comm, r, Ax, st, diag, rec, opG, opUs, opPG, opS, opABE, total;
 };
 Layout layout(const bpgl_ctx* c) {
     Carve k;
@@ -204,7 +204,6 @@ Layout layout(const bpgl_ctx* c) {
     L.st = k.take(sizeof(DevState));
     L.slab_g = k.take(8 * (int64_t)c->nchunk * c->wp);
     L.slab_s = k.take(8 * (int64_t)c->nseg * c->m);
-    L.g = k.take(8 * c->wp);
     L.D = k.take(8 * c->wp);
     L.parts = k.take(8 * 4 * (int64_t)std::max(c->nparts, c->op_tail_grid));
     L.parts2 = k.take(8 * 2 * std::max<int64_t>(kMaxReduceBlocks, c->nchunk));
@@ -833,7 +832,6 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
     p.rank = c->rank;
     p.slab_g = (double*)(s + L.slab_g);
     p.slab_s = (double*)(s + L.slab_s);
-    p.g = (double*)(s + L.g);
     p.D = (double*)(s + L.D);
     p.parts = (double*)(s + L.parts);
     p.parts2 = (double*)(s + L.parts2);

@@ -53,7 +53,6 @@ struct Params {
     int nparts, nranks, rank, has_comm;
     double* slab_g;   // [nchunk][wp]
     double* slab_s;   // [nseg][m]
-    double* g;        // [wp]
     double* D;        // [wp]
     double* parts;    // [nparts][4]   shrink partials (sum |Bx|, sum |x|, max err)
     double* parts2;   // [m/64][2]     rowreduce partials (sum r s23, sum s23^2)
@@ -347,7 +346,6 @@ __global__ __launch_bounds__(kThreads) void k_shrink(Params p) {
     double abx = 0.0, ax = 0.0, err = 0.0;
     if (j < p.wp) {
         const double g = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-        p.g[j] = g;
         double Dj = 0.0;
         if (j < p.w) {
             const double d = d_e, xj = x_e;

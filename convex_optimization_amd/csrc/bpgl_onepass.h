@@ -52,7 +52,10 @@ constexpr int kOpSlots = 1 << kOpSlotsLog;   // LDS partial slots (rows); > LAG 
 constexpr int kOpDelta = 1;     // rows between a row's phase 1 and its publication
 constexpr int kOpMaxSB = 128;   // at most two granules per lane (GPL)
 constexpr unsigned kOpPolls = 1u << 16;
-constexpr int kOpTailBlocks = 1024;   // k_onepass_tail grid cap (= its shrink partial count)
+#ifndef BPGL_TAIL_BLOCKS
+#define BPGL_TAIL_BLOCKS 1024
+#endif
+constexpr int kOpTailBlocks = BPGL_TAIL_BLOCKS;   // k_onepass_tail grid cap (= its shrink partial count)
 constexpr int kOpMaxGroups = 256;     // row groups (one block per CU: at most the CU count)
 // k_onepass_tail sums U per lane (one 64-column tile per wave) up to this many row groups; above it
 // (configs[3]: 256 groups of a 4096-column block) the 4 waves of a block split the groups of a tile
@@ -521,7 +524,7 @@ __global__ __launch_bounds__(kThreads) void k_recip(const double* __restrict__ d
 // Tail of a one-pass iteration, one kernel.  UPDATE: x += gamma D, Ax += gamma s23,
 // r = Ax - b (lasso.py:153-155, :105), g += gamma sum_groups U (fixed order); then, for every
 // mode, the shrink of the next iteration from (g, x) (lasso.py:114-119, cpu_calculation.py:
-// 15-20): D, g mirrored to p.g, and per-block [sum|Bx|, sum|x|, max err] partials that
+// 15-20): D and per-block [sum|Bx|, sum|x|, max err] partials that
 // the next line search folds (p.nparts = gridDim.x).  UPDATE = false runs the shrink alone (after a
 // reset or an exact refresh of g).  UPDATE also advances the launch parity iff k_onepass ran
 // (it runs in the iteration whose line search stops, too).
@@ -650,7 +653,6 @@ __global__ __launch_bounds__(kThreads) void k_onepass_tail(Params p, OnePassArgs
             g += gamma * u;
             o.G[j] = g;
         }
-        p.g[j] = g;
         double Dj = 0.0;
         if (j < p.w) {
             if (UPDATE) {

@@ -75,6 +75,8 @@ struct PanelState {
 struct PanelParams {
     const __bf16* A;    // [m][lda]   block b at column offset b * w
     long long lda;
+    const __bf16* At;   // pass 2's copy of A in 256 x 64 tiles, [m / 256][n / 64][256][64] (kPanelTiled2)
+    const __bf16* A1t;  // pass 1's copy of A in 64 x 256 tiles, [m / 64][n / 256][64][256] (kPanelTiled1)
     long long m, w;
     int nblock, k;
     int kchunks;        // pass-2 split of the block's w columns
@@ -192,7 +194,13 @@ __device__ __forceinline__ void panel_op_piece(int q, const __bf16* __restrict__
     if ((BPGL_PANEL_DIAG & 8) && NS == 2 && pc * 8 >= G::K) return;
     glds16o((hl ? lo : hi) + (long long)rhs * ld + ks + 8 * c, obuf + pc * 1024);
 }
-// pass-1 A stage: rows ks..ks+63 of A, columns col0..col0+255 -> [64][512 B] (a piece = 2 rows)
+// pass-1 A stage: rows ks..ks+63 of A, columns col0..col0+255 -> [64][512 B] (a piece = 2 rows).
+// kPanelTiled1 (BPGL_PANEL_T1): from p.A1t, where the stage's 64 x 256 tile is one contiguous 32 KiB
+// ([m / 64][n / 256][64][256]; `lda` is then n / 256)
+#ifndef BPGL_PANEL_T1
+#define BPGL_PANEL_T1 1
+#endif
+constexpr bool kPanelTiled1 = BPGL_PANEL_T1 != 0;
 template <int NT>
 __device__ __forceinline__ void panel_a1_piece(int q, const __bf16* __restrict__ A, long long lda, long long ks,
                                                long long col0, char* abuf, int wave, int lane) {
@@ -200,9 +208,20 @@ __device__ __forceinline__ void panel_a1_piece(int q, const __bf16* __restrict__
     const int pc = q * G::NW + wave;
     const int row = pc * 2 + (lane >> 5);
     const int c = swz512(row, lane & 31);
-    glds16a(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
+    if constexpr (kPanelTiled1)
+        glds16a(A + (((ks >> 6) * lda + (col0 >> 8)) << 14) + row * 256 + 8 * c, abuf + pc * 1024);
+    else
+        glds16a(A + (ks + row) * lda + col0 + 8 * c, abuf + pc * 1024);
 }
-// pass-2 A stage: rows r0..r0+255 of A, columns ks..ks+63 -> [256][128 B] (a piece = 8 rows)
+// pass-2 A stage: rows r0..r0+255 of A, columns ks..ks+63 -> [256][128 B] (a piece = 8 rows).
+// kPanelTiled2 (BPGL_PANEL_T2, default 1): from p.At, where the stage's 256 x 64 tile is one contiguous
+// 32 KiB ([m / 256][n / 64][256][64]; `lda` is then n / 64, the tiles per 256-row band) instead of 128 B
+// from each of 256 rows 128 KiB apart -- the pass-2 A stream alone ran at 6.0 TB/s against pass 1's
+// 6.3 (timing-only builds without the operand stream, round 5: profiles/r05/panel_diag)
+#ifndef BPGL_PANEL_T2
+#define BPGL_PANEL_T2 1
+#endif
+constexpr bool kPanelTiled2 = BPGL_PANEL_T2 != 0;
 template <int NT>
 __device__ __forceinline__ void panel_a2_piece(int q, const __bf16* __restrict__ A, long long lda, long long r0,
                                                long long ks, char* abuf, int wave, int lane) {
@@ -210,7 +229,25 @@ __device__ __forceinline__ void panel_a2_piece(int q, const __bf16* __restrict__
     const int pc = q * G::NW + wave;
     const int row = pc * 8 + (lane >> 3);
     const int c = swz128(row, lane & 7);
-    glds16a(A + (r0 + row) * lda + ks + 8 * c, abuf + pc * 1024);
+    if constexpr (kPanelTiled2)
+        glds16a(A + (((r0 >> 8) * lda + (ks >> 6)) << 14) + row * 64 + 8 * c, abuf + pc * 1024);
+    else
+        glds16a(A + (r0 + row) * lda + ks + 8 * c, abuf + pc * 1024);
+}
+// a tiled copy of A: tile (band, ct) = rows TR band .., columns TC ct .. as one contiguous TR x TC block
+// (32 KiB); a thread copies 128 B of it.  grid = (m / TR) x (n / TC).  Pass 2: TR 256, TC 64; pass 1: 64, 256
+template <int TR, int TC>
+__global__ __launch_bounds__(256) void k_panel_tile(const __bf16* __restrict__ A, long long lda, long long n,
+                                                    __bf16* __restrict__ At) {
+    static_assert(TR * TC == 256 * 64, "32 KiB tiles");
+    const long long nct = n / TC;
+    const long long band = blockIdx.x / nct, ct = blockIdx.x % nct;
+    const int r = threadIdx.x / (TC / 64), c = (threadIdx.x % (TC / 64)) * 64;
+    const __bf16* src = A + (band * TR + r) * lda + ct * TC + c;
+    __bf16* dst = At + ((long long)blockIdx.x << 14) + r * TC + c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        *reinterpret_cast<uint4*>(dst + 8 * k) = *reinterpret_cast<const uint4*>(src + 8 * k);
 }
 
 // B fragment (lane: rhs = lane & 15 of the N-tile, K = 32h + 8(lane>>4) + 0..7)
@@ -656,14 +693,18 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                         hq = *reinterpret_cast<const bf16x4*>(p.Dh + (long long)rhs * p.ldd + j);
                         lq = *reinterpret_cast<const bf16x4*>(p.Dl + (long long)rhs * p.ldd + j);
                     }
+                    bool chg = false;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         double dq = (double)(float)hq[r];
                         if constexpr (DS == 2) dq += (double)(float)lq[r];
+                        chg = chg || (dq != 0.0 && gprev != 0.0);
                         xs[r] = (float)((double)xs[r] + gprev * dq);
                     }
-                    put(p.X, ((long long)mb * p.k + rhs) * p.w + j,
-                           make_float4(xs[0], xs[1], xs[2], xs[3]));
+                    // x + gamma * 0 is x: columns the step left alone (most of a sparse solution's) keep
+                    // their stored x, which saves a share of the 32 MiB X write at configs[4]
+                    if (chg)
+                        put(p.X, ((long long)mb * p.k + rhs) * p.w + j, make_float4(xs[0], xs[1], xs[2], xs[3]));
                 }
                 __bf16 dh[4], dl[4];
                 panel_shrink4<DS, GM>(acc[mt][nt], xs, gs, dgv, rcv, mu, dh, dl, sbx, sx, err);
@@ -751,14 +792,16 @@ __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int m
                 bf16x4 hq = hq1, lq;
                 if constexpr (DS == 2) hq = *reinterpret_cast<const bf16x4*>(dptr(p.Dh, nt, mt));
                 if constexpr (DS == 2) lq = *reinterpret_cast<const bf16x4*>(dptr(p.Dl, nt, mt));
+                bool chg = false;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     double dq = (double)(float)hq[r];
                     if constexpr (DS == 2) dq += (double)(float)lq[r];
+                    chg = chg || (dq != 0.0 && gprev != 0.0);
                     xs[r] = (float)((double)xs[r] + gprev * dq);
                 }
-                put(p.X, ((long long)mb * p.k + rhs) * p.w + j,
-                       make_float4(xs[0], xs[1], xs[2], xs[3]));
+                if (chg)   // x + gamma * 0 is x: unchanged columns keep their stored x
+                    put(p.X, ((long long)mb * p.k + rhs) * p.w + j, make_float4(xs[0], xs[1], xs[2], xs[3]));
             }
             __bf16 dh[4], dl[4];
             if constexpr (DS == 2) {
@@ -800,22 +843,24 @@ __global__ __launch_bounds__((PanelGeo<NT, 2>::T)) void k_panel_pass1(PanelParam
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 3, wn = wave >> 2;
     const long long c0 = (long long)blockIdx.x * kPanelRows;             // first column of this block (in block mb)
+    const __bf16* A1 = kPanelTiled1 ? p.A1t : p.A;
+    const long long ld1 = kPanelTiled1 ? (long long)p.nblock * p.w / 256 : p.lda;
     f32x4 acc[4][G::NTW];
     if constexpr (GM == 2) {   // carried iteration: U = A^T bf16(V_{t-1}), one bf16 operand
         if constexpr (ILV >= 2)
-            panel_mainloop_pipe<NT, 1, 1>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
+            panel_mainloop_pipe<NT, 1, 1>(smem, A1, ld1, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
                                           (int)(p.m / kPanelK), acc);
         else
-            panel_mainloop<NT, 1, ILV, 1>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
+            panel_mainloop<NT, 1, ILV, 1>(smem, A1, ld1, 0, (long long)mb * p.w + c0, p.Sh, p.Sh, p.ldr, 0,
                                           (int)(p.m / kPanelK), acc);
         panel_pass1_epilogue<G::NTW, EPI, DS, 2, G::NW>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
         return;
     }
     if constexpr (ILV >= 2)
-        panel_mainloop_pipe<NT, 1, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
+        panel_mainloop_pipe<NT, 1, 2>(smem, A1, ld1, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                       (int)(p.m / kPanelK), acc);
     else
-        panel_mainloop<NT, 1, ILV, 2>(smem, p.A, p.lda, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
+        panel_mainloop<NT, 1, ILV, 2>(smem, A1, ld1, 0, (long long)mb * p.w + c0, p.Rh, p.Rl, p.ldr, 0,
                                       (int)(p.m / kPanelK), acc);
 
     panel_pass1_epilogue<G::NTW, EPI, DS, GM, G::NW>(p, mb, c0, wm, wn, G::T, acc, smem, Gout);
@@ -849,11 +894,13 @@ __global__ __launch_bounds__((PanelGeo<NT, NS>::T)) void k_panel_pass2(PanelPara
     const long long kc = p.w / p.kchunks;
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
+    const __bf16* A2 = kPanelTiled2 ? p.At : p.A;
+    const long long ld2 = kPanelTiled2 ? (long long)p.nblock * p.w / 64 : p.lda;
     if constexpr (ILV >= 2)
-        panel_mainloop_pipe<NT, 2, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
+        panel_mainloop_pipe<NT, 2, NS>(smem, A2, ld2, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);
     else
-        panel_mainloop<NT, 2, ILV, NS>(smem, p.A, p.lda, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
+        panel_mainloop<NT, 2, ILV, NS>(smem, A2, ld2, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)

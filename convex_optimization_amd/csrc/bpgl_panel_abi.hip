@@ -41,7 +41,8 @@ struct bpgl_panel {
     hipGraphExec_t gexec_ref = nullptr;   // carry_g: a graph whose first iteration is the exact-gradient one
     int fuse_update = 1;          // one block, x deferred: reduce + line search + R update in one launch ("fuse_update")
     int fuse_ok = 0;              // ... and the shape and occupancy admit it (panel_fused_geo, set at bind)
-    int fuse_grid = 256;          // its grid: at most this many blocks, k x G ("fuse_grid": 256, 512 or 1024)
+    int fuse_grid = 1024;         // its grid: at most this many blocks, k x G ("fuse_grid": 256, 512 or 1024;
+                                  // 1024 measured best with 512, +0.4 % over 256: profiles/r05/panel_fused)
     int64_t t_host = 0;           // iterations enqueued since the last reset
     int64_t n_exact = 0;          // carried gradient: exact-gradient iterations since the last reset
     int64_t ldr() const { return m; }
@@ -52,7 +53,7 @@ namespace {
 
 struct PanelLayout {
     int64_t st, Rh, Rl, Dh, Dl, X, Ax, B, R, diag, rec, Sslab, S, norms, lsp, mu, gamma, err_rhs, cnt, ready, lsdone, Gc,
-        Sh, Ec, total;
+        Sh, Ec, At, A1t, total;
 };
 PanelLayout panel_layout(const bpgl_panel* c) {
     Carve k;
@@ -84,6 +85,8 @@ PanelLayout panel_layout(const bpgl_panel* c) {
     L.Gc = k.take(carry ? 4 * kw : 0);                           // the carried gradient (fp32)
     L.Sh = k.take(carry ? 2 * (int64_t)c->k * c->ldr() : 0);     // the carried product's bf16 operand
     L.Ec = k.take(carry ? 4 * km : 0);                           // its rounding error, fed into the next one (fp32)
+    L.At = k.take(kPanelTiled2 ? 2 * c->m * c->n : 0);            // pass 2's tiled copy of A (bf16)
+    L.A1t = k.take(kPanelTiled1 ? 2 * c->m * c->n : 0);           // pass 1's tiled copy of A (bf16)
     L.total = k.off;
     return L;
 }
@@ -372,8 +375,20 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     p.Ec = (float*)(s + L.Ec);
     p.ready = (unsigned long long*)(s + L.ready);
     p.lsdone = (unsigned long long*)(s + L.lsdone);
+    p.At = kPanelTiled2 ? (const __bf16*)(s + L.At) : nullptr;
+    p.A1t = kPanelTiled1 ? (const __bf16*)(s + L.A1t) : nullptr;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(s, 0, L.total, c->stream));
+    HIP_TRY(hipMemsetAsync(s, 0, L.At, c->stream));   // everything but the tiled A copies (laid out last)
+    if (kPanelTiled2) {
+        hipLaunchKernelGGL((k_panel_tile<256, 64>), dim3((unsigned)((c->m / 256) * (c->n / 64))), dim3(256), 0,
+                           c->stream, p.A, p.lda, c->n, const_cast<__bf16*>(p.At));
+        LAUNCH_CHECK("k_panel_tile");
+    }
+    if (kPanelTiled1) {
+        hipLaunchKernelGGL((k_panel_tile<64, 256>), dim3((unsigned)((c->m / 64) * (c->n / 256))), dim3(256), 0,
+                           c->stream, p.A, p.lda, c->n, const_cast<__bf16*>(p.A1t));
+        LAUNCH_CHECK("k_panel_tile");
+    }
     panel_fuse_check(c);
     c->bound = true;
     c->have_diag = false;

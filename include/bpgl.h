@@ -306,6 +306,8 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
                       int32_t kchunks /* <= 0: automatic */, void* hip_stream);
 void bpgl_panel_destroy(bpgl_panel* ctx);
 int64_t bpgl_panel_scratch_bytes(const bpgl_panel* ctx);
+/* bind makes the passes' tiled copies of A inside the scratch (two more m x n bf16 images: each pass's
+ * 64-deep stage is then one contiguous 32 KiB); A itself must stay valid while the context is bound. */
 int bpgl_panel_bind(bpgl_panel* ctx, const void* A /* [m][lda] bf16 */, int64_t lda, void* scratch,
                     int64_t scratch_bytes);
 int bpgl_panel_diag(bpgl_panel* ctx, double* out /* nullable, n fp64 */);
@@ -335,7 +337,14 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * on the objective (the gradient pass, hi + lo always, sets the fixed point;
  * profiles/r04/accuracy); short runs follow slightly different trajectories.
  * bpgl_panel_mtm / _mm always use hi + lo operands.  bpgl_panel_get_tuning reads
- * "interleave1", "interleave2", "d_split", "defer_x", "carry_g", "g_refresh".
+ * "interleave1", "interleave2", "d_split", "defer_x", "carry_g", "g_refresh", "fuse_update",
+ * "fuse_grid".
+ * "fuse_update" (0 / 1; default 1; in effect with one feature block, defer_x and m a multiple of
+ * 1024 -- get_tuning reports the form in effect; a reset must follow a change): the split-K reduce, each
+ * RHS's line search and R += gamma S run as ONE launch whose blocks wait for their RHS's step size
+ * (bitwise the two-kernel result); it needs its blocks co-resident, which bpgl_panel_bind checks with
+ * the occupancy API -- should a wait still run out (another kernel holding CUs), nothing is updated and
+ * bpgl_panel_status returns BPGL_E_EXCHANGE.  "fuse_grid" (256 / 512 / 1024, default 1024): its grid.
  * "defer_x" (0 / 1; default 1, one feature block; a reset must follow a change): the
  * update x += gamma D' of an iteration is applied by the next pass-1 epilogue (and at
  * the end of every bpgl_panel_step), bitwise the same x.

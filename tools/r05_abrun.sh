@@ -16,6 +16,9 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     BPGL_LIB=build_ab/$v.so timeout -k 10 200 $B --comm --shard rows --m 1024 --n-per-gpu 65536 --steps 256 --warmup 100 \
         --windows 5 > $OUT/m1024_${v}_$r.json 2> $OUT/m1024_${v}_$r.err || exit $?
     BPGL_LIB=build_ab/$v.so timeout -k 10 200 $B --steps 256 --warmup 100 --windows 5 ${EXTRA} > $OUT/c1_${v}_$r.json 2> $OUT/c1_${v}_$r.err || exit $?
+    if [ -n "$C3" ]; then
+      BPGL_LIB=build_ab/$v.so timeout -k 10 200 $B --config 3 --steps 64 --warmup 20 --windows 3 > $OUT/c3_${v}_$r.json 2> $OUT/c3_${v}_$r.err || exit $?
+    fi
     if [ -n "$WEAK" ]; then
       BPGL_LIB=build_ab/$v.so timeout -k 10 200 $B --comm --shard rows --m 1024 --n-per-gpu 524288 --steps 256 --warmup 50 \
           --windows 3 > $OUT/m1024w_${v}_$r.json 2> $OUT/m1024w_${v}_$r.err || exit $?

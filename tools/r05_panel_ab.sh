@@ -8,8 +8,12 @@ mkdir -p $OUT
     -k "fused or interleave or carried" > $OUT/pytest_panel.txt 2>&1 || exit $?
 B="python3 bench.py --no-cpu --no-side-legs --config 4 --steps 256 --warmup 200 --windows 5"
 for r in 1 2; do
-  for f in ${FORMS:-"0 1"}; do   # 0: two kernels; G: the fused launch on a grid of G blocks
-    if [ "$f" = 0 ]; then a="--fuse-update 0"; else a="--fuse-update 1 --fuse-grid $f"; fi
-    timeout -k 10 200 $B $a > $OUT/c4_f${f}_$r.json 2> $OUT/c4_f${f}_$r.err || exit $?
+  # LIB@G: LIB = "tree" (the in-tree library) or a build_ab/LIB.so; G = 0: two kernels, else the fused
+  # launch on a grid of G blocks
+  for f in ${FORMS:-"tree@0 tree@256"}; do
+    lib=${f%@*}; g=${f#*@}
+    if [ "$g" = 0 ]; then a="--fuse-update 0"; else a="--fuse-update 1 --fuse-grid $g"; fi
+    if [ "$lib" = tree ]; then env=""; else env="BPGL_LIB=build_ab/$lib.so"; fi
+    env $env timeout -k 10 200 $B $a > $OUT/c4_${lib}_g${g}_$r.json 2> $OUT/c4_${lib}_g${g}_$r.err || exit $?
   done
 done
