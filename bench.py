@@ -743,6 +743,10 @@ def measure_panel(args):
             "launch_mode": f"hipGraph replay, median of {args.windows} windows of {args.steps} iterations (value); "
                            f"eager + HIP events over {n_ev} iterations (kernel times)",
             "windows_s": wins,
+            # the rate depends on the iterate: early in a solve x changes in every column and pass 1
+            # stores all of X; later it skips the tiles the step left alone (pass 2 measured 201 µs at
+            # iterations 5-517, 184 µs at 1500-2012)
+            "windows_from_iteration": args.warmup + n_ev,
             "kernel_avg_ms": kms, "status": st,
         },
         "roofline": {
@@ -860,6 +864,7 @@ def panel_leg(args):
             "warmup": p["warmup"], "ms_per_step": p["ms_per_step"], "dtype": p["dtype"],
             "rhs_iters_per_s": c["rhs_iters_per_s"], "iter_roofline_frac": c["iter_roofline_frac"],
             "hbm_roofline_iters_per_s": c["hbm_roofline_iters_per_s"], "windows_s": c["windows_s"],
+            "windows_from_iteration": c["windows_from_iteration"],
             "kernel_avg_ms": c["kernel_avg_ms"], "status": c["status"],
             "tuning": {q: c[q] for q in ("d_split", "carry_g", "g_refresh", "defer_x", "fuse_update", "kchunks",
                                          "interleave12")},

@@ -68,7 +68,7 @@ def main():
     data = {}
     if os.path.exists(path):
         data = json.load(open(path))
-    data[key] = out
+    data.setdefault(key, {}).update(out)   # kernels of this key not in these passes keep their entries
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps({key: out}, indent=1))
 
