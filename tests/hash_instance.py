@@ -88,20 +88,23 @@ def np_b(A, chunk_rows=None):
 
 
 # ---------------------------------------------------------------- torch (on the GPU box)
-def torch_A(m, n, device, chunk_rows=None):
+def torch_A(m, n, device, chunk_rows=None, row0=0):
+    """rows [row0, row0 + m) of the instance's A (row0 > 0: one rank's row shard)"""
     import torch
     chunk_rows = chunk_rows or max(1, (1 << 26) // n)
     A = torch.empty((m, n), dtype=torch.float32, device=device)
     sc = 2.0 ** -24 * a_scale(n)
     for i0 in range(0, m, chunk_rows):
         i1 = min(m, i0 + chunk_rows)
-        idx = torch.arange(i0 * n, i1 * n, dtype=torch.int64, device=device)
+        idx = torch.arange((row0 + i0) * n, (row0 + i1) * n, dtype=torch.int64, device=device)
         u = (_hash(idx, SEED_A) >> 8) - (1 << 23)
         A[i0:i1] = (u.to(torch.float32) * sc).reshape(i1 - i0, n)
     return A
 
 
-def torch_b(A, chunk_rows=None):
+def torch_b(A, chunk_rows=None, row0=0, m_total=None):
+    """b of A's rows; for a row shard (A = rows [row0, row0 + m) of an m_total-row instance) the
+    shard's entries of the whole instance's b"""
     import torch
     m, n = A.shape
     dev = A.device
@@ -111,7 +114,8 @@ def torch_b(A, chunk_rows=None):
     for i0 in range(0, m, chunk_rows):
         i1 = min(m, i0 + chunk_rows)
         b[i0:i1] = A[i0:i1].double() @ x
-    return b + torch.from_numpy(np_e(m)).to(dev)
+    e = np_e(m_total or m)[row0:row0 + m]
+    return b + torch.from_numpy(e).to(dev)
 
 
 def sample_points(m, n, k=4096, seed=7):

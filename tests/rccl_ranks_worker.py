@@ -7,6 +7,8 @@ The data path is the product's: libbpgl's communicator, the all-reduce issued on
 stream.
 
 usage: rccl_ranks_worker.py CASE SHARD OUTDIR [--cumask] [--fail-rank R --fail-at T]
+  CASE: a reference fixture of tests/golden, or longrun_<config> (a full-size long-horizon fixture,
+        row shards only: see longrun())
   SHARD: columns | rows
   --cumask: the rank's solver stream gets a disjoint, XCD-symmetric 1/WORLD_SIZE of the CUs
             (distributed.xcd_symmetric_cu_mask), so each rank's persistent one-pass grid is
@@ -47,6 +49,8 @@ def main():
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
     fx = dict(np.load(os.path.join(ROOT, "tests", "golden", a.case + ".npz")))
+    if a.case.startswith("longrun_"):
+        return longrun(a, fx, rank, world, np, torch, dist, D, GPU_Calculation)
     A = oracle.fixture_A(fx)
     block, iters = int(fx["BLOCK"]), int(fx["ITER_MAX"])
     eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
@@ -84,6 +88,44 @@ def main():
         out[f"onepass_{tag}"] = np.int64(gc.solver_stat("onepass"))
     out["diag"] = np.asarray(gc.diag_ATA).reshape(-1)
     out["fallbacks"] = out["fallbacks_eager"]
+    np.savez(os.path.join(a.outdir, f"rank{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def longrun(a, fx, rank, world, np, torch, dist, D, GPU_Calculation):
+    """A full-size long-horizon fixture (tests/golden/longrun_*.npz: the C oracle's x after ITER
+    iterations on the hash instance of tests/hash_instance.py) over WORLD_SIZE RCCL row ranks: each
+    rank builds its own rows in HBM, proves them (the fixture's A samples in its rows; b's SHA-256
+    over the gathered shards) and runs the whole horizon in graph replay."""
+    import hashlib
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import hash_instance as H
+
+    m, n, iters, mu = int(fx["m"]), int(fx["n"]), int(fx["iters"]), float(fx["mu"])
+    s, e = D.row_bounds(m, rank, world)
+    A = H.torch_A(e - s, n, "cuda:0", row0=s)
+    rows, cols = fx["A_rows"], fx["A_cols"]
+    mine = (rows >= s) & (rows < e)
+    got = A[torch.from_numpy(rows[mine] - s).cuda(), torch.from_numpy(cols[mine]).cuda()].cpu().numpy()
+    samples_ok = bool(np.array_equal(got, fx["A_samples"][mine]))
+    b = H.torch_b(A, row0=s, m_total=m)
+    parts = [None] * world
+    dist.all_gather_object(parts, b.cpu().numpy())
+    b_ok = hashlib.sha256(np.concatenate(parts).tobytes()).hexdigest() == str(fx["b_sha256"])
+    GC = type("GC_float", (GPU_Calculation,), {"TYPE": "float"})
+    mask = D.xcd_symmetric_cu_mask(rank, world, torch.cuda.get_device_properties(0).multi_processor_count) \
+        if a.cumask else None
+    gc = GC(A, 1, device=0, comm=D.RankComm(rank, world), shard="rows", cu_mask=mask)
+    torch.cuda.synchronize()
+    dist.barrier()
+    res = gc.run(b, mu, iters, record=True, use_graph=True)
+    out = {"x": np.asarray(res["x"]).reshape(-1), "err": np.asarray(res["err_iter"]),
+           "iters": np.int64(res["iters"]), "samples_ok": np.bool_(samples_ok), "b_ok": np.bool_(b_ok),
+           "in_place": np.bool_(gc._A_dev.data_ptr() == A.data_ptr()),
+           "onepass": np.int64(gc.solver_stat("onepass")), "fallbacks": np.int64(gc.solver_stat("fallbacks")),
+           "refreshes": np.int64(gc.solver_stat("refreshes")), "cus": np.int64(gc.solver_stat("cus"))}
     np.savez(os.path.join(a.outdir, f"rank{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()

@@ -28,6 +28,18 @@ def test_numpy_and_torch_agree_bitwise():
     assert all(np.array_equal(B[:, r].numpy(), H.np_b_rhs(Ab, r)) for r in range(3))
 
 
+def test_row_shards_are_slices_of_the_instance():
+    """torch_A / torch_b of a row shard (the RCCL long-horizon test's ranks build only their rows) are
+    the rows of the whole instance's A and b, bit for bit"""
+    import torch
+    A = H.np_A(300, 1000)
+    b = H.np_b(A)
+    for r0, r1 in ((0, 150), (150, 300), (7, 11)):
+        As = H.torch_A(r1 - r0, 1000, "cpu", chunk_rows=3, row0=r0)
+        assert torch.equal(As, torch.from_numpy(A[r0:r1]))
+        assert np.array_equal(H.torch_b(As, row0=r0, m_total=300).numpy(), b[r0:r1])
+
+
 def test_b_is_exact_in_any_order():
     A = H.np_A(200, 4096)
     x = H.np_x_true(4096)
