@@ -136,6 +136,8 @@ def parse():
                     help="largest hipGraph of iterations replayed (power of two; -1: library default, 64)")
     ap.add_argument("--onepass-cache", type=int, default=-1,
                     help="permille of each one-pass row group read with cache-allocating loads (-1: library default)")
+    ap.add_argument("--onepass-rows", type=int, default=-1, choices=[-1, 0, 1],
+                    help="one-pass row groups: 1 interleaved rows, 0 consecutive (-1: library default)")
     ap.add_argument("--comm", action="store_true",
                     help="attach an RCCL communicator even at N = 1 (runs the sharded/all-reduce leg)")
     ap.add_argument("--shard", default="auto", choices=["auto", "rows", "columns"],
@@ -339,6 +341,8 @@ def measure(ctx, args, m, n_total):
         gc.set_tuning("tail_row_blocks", args.tail_row_blocks)
     if args.onepass_cache >= 0:
         gc.set_tuning("onepass_cache_permille", args.onepass_cache)
+    if args.onepass_rows >= 0:
+        gc.set_tuning("onepass_rows", args.onepass_rows)
     if args.graph_max > 0:
         gc.set_tuning("graph_max", args.graph_max)
 
@@ -391,7 +395,7 @@ def measure(ctx, args, m, n_total):
     return dict(gc=gc, windows=wins, el_events=el_ev, n_events=n_ev, kernel_ms=times, samples=samples, status=st,
                 refresh_ms=refresh_ms, refresh_period=period, w_local=gc.MAT_WIDTH, m_local=gc.MAT_HEIGHT,
                 b=b, mu=mu, fallbacks=gc.solver_stat("fallbacks"), onepass=gc.solver_stat("onepass"),
-                attempts=attempt + 1, cus=gc.solver_stat("cus"))
+                attempts=attempt + 1, cus=gc.solver_stat("cus"), onepass_rows=gc.solver_stat("onepass_rows"))
 
 
 def window_rate(res, K):
@@ -1071,6 +1075,7 @@ def main():
         out["cpu_baseline"]["pool_configs0"] = pool
     out["config"]["measure_attempts"] = res["attempts"]
     out["config"]["cus_per_rank"] = res["cus"]
+    out["config"]["onepass_rows"] = "interleaved" if res["onepass_rows"] else "consecutive"
     if G > 1 and not args.no_strong:
         # the other legs of one SCALE run: the other scaling form (weak:
         # configs[2]'s shape, or strong when --weak made the weak problem the value line), the

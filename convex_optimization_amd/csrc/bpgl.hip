@@ -117,6 +117,7 @@ struct bpgl_ctx {
     int op_refresh = 256;
     // permille of each row group read with cache-allocating loads (-1: auto, op_cache_auto)
     int op_cache = -1;
+    int op_rows = -1;          // tuning "onepass_rows": -1 auto, 0 consecutive, 1 interleaved
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
     int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
@@ -192,6 +193,17 @@ int op_cache_eff(const bpgl_ctx* c) {
     if (c->op_cache >= 0) return c->op_cache;
     const int64_t bytes = c->m * c->wp * (c->dtype == BPGL_F32 ? 4 : c->dtype == BPGL_F64 ? 8 : 2);
     return bytes <= (int64_t)320 << 20 ? 750 : 0;
+}
+
+// "onepass_rows" = -1 (default): row groups own interleaved rows (g, g + ngroups, ...) when the groups
+// are many and long -- configs[1] (16 groups of 512 rows, 16 segment blocks): k_onepass 334.0 -> 329.6 us,
+// the groups then read one contiguous window of A instead of 16 streams 128 MiB apart -- and consecutive
+// rows otherwise: interleaving measured slower at 64-row groups (the N = 8 strong shard, 51.6 -> 52.9 us),
+// with one segment block per row (configs[3], 2709 -> 2757 us) and at 2 groups (the weak shard, 328 ->
+// 333.7 us); profiles/r05/layout.  Results agree to rounding (the U partials sum other rows per group).
+int op_rows_eff(const bpgl_ctx* c) {
+    if (c->op_rows >= 0) return c->op_rows;
+    return c->op_SB >= 16 && c->op_ngroups >= 8 && c->op_R >= 512 ? 1 : 0;
 }
 
 // scratch layout (offsets in bytes)
@@ -695,7 +707,7 @@ int recover_onepass(bpgl_ctx* c, DevState& st) {
 extern "C" {
 
 const char* bpgl_last_error(void) { return bpgl_host::g_err.c_str(); }
-int bpgl_version(void) { return 300; }
+int bpgl_version(void) { return 301; }
 
 int bpgl_stream_create(int device, const uint32_t* cu_mask, int32_t mask_words, void** out) {
     if (!out) return fail(BPGL_E_ARG, "out is null");
@@ -859,6 +871,7 @@ int bpgl_bind(bpgl_ctx* c, const void* A, int64_t lda, int64_t block_stride, voi
         c->op.ls = c->rows ? 0 : 1;   // row shards: the line search follows the all-reduce (in the tail)
         c->op.abe = c->rows ? (double*)(s + L.opABE) : nullptr;
         c->op.cache_permille = op_cache_eff(c);
+        c->op.rilv = op_rows_eff(c);
     }
     c->op.fail_at = c->op_fail_at;
     HIP_TRY(hipSetDevice(c->device));
@@ -1122,6 +1135,7 @@ int bpgl_solver_stat(bpgl_ctx* c, const char* key, int64_t* value) {
     else if (!strcmp(key, "cus")) *value = c->cus;
     else if (!strcmp(key, "cu_masked")) *value = c->cu_masked ? 1 : 0;
     else if (!strcmp(key, "onepass_grid")) *value = (int64_t)c->op_ngroups * c->op_SB;
+    else if (!strcmp(key, "onepass_rows")) *value = c->op_shape ? op_rows_eff(c) : 0;
     else return fail(BPGL_E_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1183,6 +1197,14 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
         if (value < -1 || value > 1000) return fail(BPGL_E_ARG, "onepass_cache_permille must be -1 (auto) or in [0, 1000]");
         c->op_cache = (int)value;
         c->op.cache_permille = op_cache_eff(c);
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "onepass_rows")) {
+        if (value < -1 || value > 1) return fail(BPGL_E_ARG, "onepass_rows must be -1 (auto), 0 or 1");
+        c->op_rows = (int)value;
+        if (c->op_shape) c->op.rilv = op_rows_eff(c);
         drop_graphs(c);
         c->solver = false;
         return 0;

@@ -74,6 +74,7 @@ struct OnePassArgs {
     long long fail_at;           // test hook: iteration whose launch reports a hand-off failure (-1: none)
     int rowb;                    // k_onepass_tail: blocks appended after the column blocks that only run
                                  // the residual update (0: the column blocks run it first, as before)
+    int rilv;                    // 1: row group g owns rows g, g + ngroups, ... (interleaved), 0: R consecutive rows
     int tailw;                   // k_onepass_tail, one rank: every lane sums its column's U partials itself
                                  // (wave-owned 64-column tiles, no LDS fold; ngroups <= kOpTailWaveGroups)
 };
@@ -215,14 +216,18 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     int grp, sb;
     if (o.xl) { grp = (b & 7) + 8 * ((b >> 3) / SB); sb = (b >> 3) % SB; }
     else { grp = b / SB; sb = b % SB; }
-    const long long i0 = (long long)grp * o.R;
+    // this group's rows: R consecutive ones, or (rilv) rows grp, grp + ngroups, ... -- the groups then
+    // read adjacent rows at once (one contiguous window of A instead of ngroups streams R rows apart)
+    const long long gs = o.rilv ? o.ngroups : 1;
+    const long long i0 = o.rilv ? grp : (long long)grp * o.R;
     const long long i1 = i0 + o.R < p.m ? i0 + o.R : p.m;
+    const int nrows = o.rilv ? (grp < p.m ? (int)((p.m - grp + gs - 1) / gs) : 0) : (i1 > i0 ? (int)(i1 - i0) : 0);
+    auto rowat = [&](long long i) -> long long { return i0 + i * gs; };   // this group's i-th row
     // launches alternate the row direction; each reads the last cache_permille of its rows with
     // cache-allocating loads, which the next launch (opposite direction) reads first from the
     // Infinity Cache (only the small tail kernel runs in between)
     const bool rev = ((p.st->op_epoch - p.st->op_base) & 1) != 0;   // per solver run: reruns repeat bits
-    auto rowof = [&](int t) -> long long { return rev ? i1 - 1 - t : i0 + t; };
-    const int nrows = i1 > i0 ? (int)(i1 - i0) : 0;
+    auto rowof = [&](int t) -> long long { return rowat(rev ? nrows - 1 - t : t); };
     if (nrows == 0) {   // the whole row group (uniform); ngroups = cdiv(m, R) makes this unreachable
         if (sb == 0 && threadIdx.x == 0) { st_sc1(p.parts2 + 2ll * grp, 0.0); st_sc1(p.parts2 + 2ll * grp + 1, 0.0); }
         if (o.ls && op_arrive_last(&p.st->op_cnt, (unsigned long long)gridDim.x)) op_linesearch(p, o.ngroups);
@@ -395,8 +400,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             double sv[8], rv[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                sv[k] = o.S[i0 + i + 64 * k];
-                rv[k] = p.r[i0 + i + 64 * k];
+                sv[k] = o.S[rowat(i + 64 * k)];
+                rv[k] = p.r[rowat(i + 64 * k)];
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -405,8 +410,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             }
         }
         for (; i < nrows; i += 64) {
-            const double sv = o.S[i0 + i];
-            rs = fma(p.r[i0 + i], sv, rs);
+            const double sv = o.S[rowat(i)];
+            rs = fma(p.r[rowat(i)], sv, rs);
             ss = fma(sv, sv, ss);
         }
         rs = op_wave_sum(rs);

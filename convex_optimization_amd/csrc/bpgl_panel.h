@@ -75,7 +75,7 @@ struct PanelState {
 struct PanelParams {
     const __bf16* A;    // [m][lda]   block b at column offset b * w
     long long lda;
-    const __bf16* At;   // pass 2's copy of A in 256 x 64 tiles, [m / 256][n / 64][256][64] (kPanelTiled2)
+    const __bf16* At;   // pass 2's copy of A in 256 x 64 tiles, [n / 64][m / 256][256][64] (kPanelTiled2)
     const __bf16* A1t;  // pass 1's copy of A in 64 x 256 tiles, [m / 64][n / 256][64][256] (kPanelTiled1)
     long long m, w;
     int nblock, k;
@@ -215,9 +215,11 @@ __device__ __forceinline__ void panel_a1_piece(int q, const __bf16* __restrict__
 }
 // pass-2 A stage: rows r0..r0+255 of A, columns ks..ks+63 -> [256][128 B] (a piece = 8 rows).
 // kPanelTiled2 (BPGL_PANEL_T2, default 1): from p.At, where the stage's 256 x 64 tile is one contiguous
-// 32 KiB ([m / 256][n / 64][256][64]; `lda` is then n / 64, the tiles per 256-row band) instead of 128 B
-// from each of 256 rows 128 KiB apart -- the pass-2 A stream alone ran at 6.0 TB/s against pass 1's
-// 6.3 (timing-only builds without the operand stream, round 5: profiles/r05/panel_diag)
+// 32 KiB, the tiles stage-major ([n / 64][m / 256][256][64]; `lda` is then m / 256, the tiles per column
+// strip): the 32 row bands of a column chunk read one contiguous 1 MiB per stage, as pass 1's blocks read
+// one 8 MiB window.  Measured against 128 B from each of 256 rows 128 KiB apart (untiled) and against the
+// tiles band-major (each block streaming its own 4 MiB, 256 streams 4 MiB apart): pass 2 184.4 -> 170.4
+// µs, configs[4] 2583 -> 2670 it/s (round 5: profiles/r05/panel_tiles, profiles/r05/layout)
 #ifndef BPGL_PANEL_T2
 #define BPGL_PANEL_T2 1
 #endif
@@ -230,21 +232,23 @@ __device__ __forceinline__ void panel_a2_piece(int q, const __bf16* __restrict__
     const int row = pc * 8 + (lane >> 3);
     const int c = swz128(row, lane & 7);
     if constexpr (kPanelTiled2)
-        glds16a(A + (((r0 >> 8) * lda + (ks >> 6)) << 14) + row * 64 + 8 * c, abuf + pc * 1024);
+        glds16a(A + (((ks >> 6) * lda + (r0 >> 8)) << 14) + row * 64 + 8 * c, abuf + pc * 1024);
     else
         glds16a(A + (r0 + row) * lda + ks + 8 * c, abuf + pc * 1024);
 }
 // a tiled copy of A: tile (band, ct) = rows TR band .., columns TC ct .. as one contiguous TR x TC block
-// (32 KiB); a thread copies 128 B of it.  grid = (m / TR) x (n / TC).  Pass 2: TR 256, TC 64; pass 1: 64, 256
-template <int TR, int TC>
+// (32 KiB); a thread copies 128 B of it.  grid = (m / TR) x (n / TC).  Tiles in the order their pass's stages
+// run: pass 1 (TR 64, TC 256) band-major -- a band is one stage --, pass 2 (TR 256, TC 64, CM) column-major
+template <int TR, int TC, bool CM>
 __global__ __launch_bounds__(256) void k_panel_tile(const __bf16* __restrict__ A, long long lda, long long n,
                                                     __bf16* __restrict__ At) {
     static_assert(TR * TC == 256 * 64, "32 KiB tiles");
-    const long long nct = n / TC;
+    const long long nct = n / TC, nband = (long long)gridDim.x / nct;
     const long long band = blockIdx.x / nct, ct = blockIdx.x % nct;
     const int r = threadIdx.x / (TC / 64), c = (threadIdx.x % (TC / 64)) * 64;
     const __bf16* src = A + (band * TR + r) * lda + ct * TC + c;
-    __bf16* dst = At + ((long long)blockIdx.x << 14) + r * TC + c;
+    // CM: tile (band, ct) at ct * nband + band (column tiles major), else band * nct + ct
+    __bf16* dst = At + ((CM ? ct * nband + band : (long long)blockIdx.x) << 14) + r * TC + c;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         *reinterpret_cast<uint4*>(dst + 8 * k) = *reinterpret_cast<const uint4*>(src + 8 * k);
@@ -895,7 +899,7 @@ __global__ __launch_bounds__((PanelGeo<NT, NS>::T)) void k_panel_pass2(PanelPara
     const long long r0 = (long long)rb * kPanelRows;
     f32x4 acc[4][G::NTW];
     const __bf16* A2 = kPanelTiled2 ? p.At : p.A;
-    const long long ld2 = kPanelTiled2 ? (long long)p.nblock * p.w / 64 : p.lda;
+    const long long ld2 = kPanelTiled2 ? p.m / 256 : p.lda;
     if constexpr (ILV >= 2)
         panel_mainloop_pipe<NT, 2, NS>(smem, A2, ld2, r0, (long long)mb * p.w + chunk * kc, p.Dh, p.Dl, p.ldd,
                                        chunk * kc, (int)(kc / kPanelK), acc);

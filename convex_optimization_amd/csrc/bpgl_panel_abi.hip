@@ -380,12 +380,12 @@ int bpgl_panel_bind(bpgl_panel* c, const void* A, int64_t lda, void* scratch, in
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(s, 0, L.At, c->stream));   // everything but the tiled A copies (laid out last)
     if (kPanelTiled2) {
-        hipLaunchKernelGGL((k_panel_tile<256, 64>), dim3((unsigned)((c->m / 256) * (c->n / 64))), dim3(256), 0,
+        hipLaunchKernelGGL((k_panel_tile<256, 64, true>), dim3((unsigned)((c->m / 256) * (c->n / 64))), dim3(256), 0,
                            c->stream, p.A, p.lda, c->n, const_cast<__bf16*>(p.At));
         LAUNCH_CHECK("k_panel_tile");
     }
     if (kPanelTiled1) {
-        hipLaunchKernelGGL((k_panel_tile<64, 256>), dim3((unsigned)((c->m / 64) * (c->n / 256))), dim3(256), 0,
+        hipLaunchKernelGGL((k_panel_tile<64, 256, false>), dim3((unsigned)((c->m / 64) * (c->n / 256))), dim3(256), 0,
                            c->stream, p.A, p.lda, c->n, const_cast<__bf16*>(p.A1t));
         LAUNCH_CHECK("k_panel_tile");
     }

@@ -63,7 +63,8 @@ const char* bpgl_last_error(void);
  *   300 (0.3.0): the opt-in forms measured to lose were removed:
  *                tuning keys "fused", "onepass_fold", "onepass_variant"; panel keys "lo8",
  *                "r_refresh", "write_through", "op_pad", "waves*", interleave 3; panel stat
- *                "refreshes"; bpgl_panel_refresh. */
+ *                "refreshes"; bpgl_panel_refresh.
+ *   301 (0.3.1): tuning key "onepass_rows" and solver stat "onepass_rows". */
 int bpgl_version(void);
 
 /*
@@ -216,7 +217,8 @@ double* bpgl_solver_exchange_buffer(bpgl_ctx* ctx, int64_t* count);
  *   enqueued), "fallbacks" (recoveries above), "requested"
  *   (iterations asked of bpgl_solver_step), "enqueued", "cus" (CUs the
  *   persistent grid is sized for), "cu_masked" (1: narrower than the device,
- *   from the stream's CU mask), "onepass_grid" (its blocks).
+ *   from the stream's CU mask), "onepass_grid" (its blocks), "onepass_rows" (1:
+ *   the row groups own interleaved rows, see "onepass_rows" under bpgl_set_tuning).
  * bpgl_solver_residual: device pointer of the residual s11 = sum_k Ax_k - b (m).
  */
 int bpgl_solver_reset(bpgl_ctx* ctx, const double* b, double mu, double* x,
@@ -272,6 +274,11 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   at most 320 MiB, i.e. about the 256 MiB Infinity Cache, else 0): share of every
  *   row group the one-pass kernel reads with cache-allocating loads (launches
  *   alternate the row direction, so the next launch starts on those rows).
+ *   "onepass_rows" (default -1 = auto: interleaved when there are at least 8 row
+ *   groups of at least 512 rows over at least 16 segment blocks, else 0): 1 = row
+ *   group g of the one-pass kernel owns rows g, g + ngroups, ... (the groups read
+ *   adjacent rows at once), 0 = R consecutive rows; bpgl_solver_stat("onepass_rows")
+ *   reports the form in use.
  *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for

@@ -100,6 +100,34 @@ def test_shapes_match_two_pass_and_oracle(m, n, type_name):
         assert rel(one["x"], ref["x"]) <= 1e-8, rel(one["x"], ref["x"])
 
 
+@pytest.mark.parametrize("m,n,type_name", [(1000, 4100, "float"), (37, 9000, "float"), (4099, 1536, "float"),
+                                            (777, 3000, "double"), (1500, 10000, "bf16"), (300, 64 * 4096, "bf16")])
+def test_interleaved_row_groups(m, n, type_name):
+    """"onepass_rows" 1 (row group g owns rows g, g + ngroups, ...; the default at configs[1]) and 0
+    (R consecutive rows) against the two-pass path, at the tolerances above (the U partials and the
+    line-search shares sum other rows per group: rounding only); graph = eager bitwise; the stat
+    reports the form in use; the stop rule stops at the same iteration"""
+    rs = np.random.RandomState(m + 3 * n)
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * np.abs(A.T @ b).max()
+    gc = make_cls(type_name)(A, 1, device=0)
+    gc.set_tuning("onepass", 0)
+    two5, two25 = gc.run(b, mu, 5)["x"], gc.run(b, mu, 25)["x"]
+    gc.set_tuning("onepass", 1)
+    for rows in (1, 0):
+        gc.set_tuning("onepass_rows", rows)
+        r5 = gc.run(b, mu, 5)
+        assert gc.solver_stat("onepass") == 1 and gc.solver_stat("onepass_rows") == rows
+        assert rel(r5["x"], two5) <= 1e-12, (rows, rel(r5["x"], two5))
+        g = gc.run(b, mu, 25, use_graph=True)["x"]
+        e = gc.run(b, mu, 25, use_graph=False)["x"]
+        np.testing.assert_array_equal(g, e)
+        assert rel(g, two25) <= 1e-8, (rows, rel(g, two25))
+    with pytest.raises(N.BpglError):
+        gc.set_tuning("onepass_rows", 2)
+
+
 def test_graph_eager_split_steps_bitwise():
     rs = np.random.RandomState(5)
     A = rs.randn(900, 5000)
@@ -212,6 +240,7 @@ def test_full_size_matches_oracle():
     gc, b, mu, _ = device_instance(8192, 65536, 0.4, 1, TYPE="float", seed=11, device=0)
     assert used_onepass(gc, b, mu)
     res = gc.run(b, mu, 8)
+    assert gc.solver_stat("onepass_rows") == 1   # the default here: interleaved row groups
     A_host = gc.A_b_gpu[0].cpu().numpy()
     ref = oracle.run(np.ascontiguousarray(A_host), b.cpu().numpy(), mu, 1, 8, nthreads=16)
     assert rel(res["x"], ref["x"]) <= 1e-5

@@ -44,7 +44,7 @@ def _exchange(ranks, fp32=False):
     torch.cuda.synchronize()
 
 
-def run_external(A, b, mu, world, iters, type_name="float", err_bound=None, refresh=64, fp32=False):
+def run_external(A, b, mu, world, iters, type_name="float", err_bound=None, refresh=64, fp32=False, rows=-1):
     """`world` row-shard ranks on one GPU, the all-reduce done here (``fp32``: the fp32 wire
     format of phases 0/1, summed in fp32 like RCCL)."""
     ranks = []
@@ -53,6 +53,7 @@ def run_external(A, b, mu, world, iters, type_name="float", err_bound=None, refr
         gc.set_ranks(g, world)
         gc.set_tuning("onepass_refresh", refresh)
         gc.set_tuning("exchange_fp32", 1 if fp32 else 0)
+        gc.set_tuning("onepass_rows", rows)
         ranks.append(gc)
     diag = sum(gc._diag.clone() for gc in ranks)   # column norms: sums over ranks
     for g, gc in enumerate(ranks):
@@ -114,6 +115,31 @@ def test_external_row_ranks_match_reference(golden, case, world, type_name):
     errs = [gc.solver_records()[0] for gc in ranks]
     np.testing.assert_array_equal(errs[0], errs[-1])
     np.testing.assert_allclose(errs[0][:IT], fx["err_iter"][:IT], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_external_row_ranks_interleaved_row_groups(world):
+    """every rank's row groups on interleaved rows ("onepass_rows" 1; 3 ranks: ragged shards of 3001
+    rows, 5 segment blocks per row, ~50 row groups of ~20 rows per rank): ranks bit-identical, within
+    1e-10 of the consecutive-row form and of the single-rank solver, and 1e-8 of the oracle"""
+    rs = np.random.RandomState(31)
+    m, n = 3001, 20000
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * float(np.abs(A.T @ b).max())
+    IT = 25
+    ilv = run_external(A, b, mu, world, IT, rows=1)
+    con = run_external(A, b, mu, world, IT, rows=0)
+    assert all(gc.solver_stat("onepass_rows") == 1 for gc in ilv)
+    assert all(gc.solver_stat("onepass_rows") == 0 for gc in con)
+    xs = [gc.solver_x() for gc in ilv]
+    for x in xs[1:]:
+        np.testing.assert_array_equal(x, xs[0])
+    single = make_cls("float")(A, 1, device=0).run(b, mu, IT)["x"]
+    orc = oracle.run(A.astype(np.float32).astype(np.float64), b, mu, 1, IT)["x"]
+    assert rel(xs[0], con[0].solver_x()) <= 1e-10, rel(xs[0], con[0].solver_x())
+    assert rel(xs[0], single) <= 1e-10, rel(xs[0], single)
+    assert rel(xs[0], orc) <= 1e-8, rel(xs[0], orc)
 
 
 def test_external_row_ranks_ragged_and_stop():
