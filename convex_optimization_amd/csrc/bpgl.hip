@@ -195,15 +195,17 @@ int op_cache_eff(const bpgl_ctx* c) {
     return bytes <= (int64_t)320 << 20 ? 750 : 0;
 }
 
-// "onepass_rows" = -1 (default): row groups own interleaved rows (g, g + ngroups, ...) when the groups
-// are many and long -- configs[1] (16 groups of 512 rows, 16 segment blocks): k_onepass 334.0 -> 329.6 us,
-// the groups then read one contiguous window of A instead of 16 streams 128 MiB apart -- and consecutive
-// rows otherwise: interleaving measured slower at 64-row groups (the N = 8 strong shard, 51.6 -> 52.9 us),
-// with one segment block per row (configs[3], 2709 -> 2757 us) and at 2 groups (the weak shard, 328 ->
-// 333.7 us); profiles/r05/layout.  Results agree to rounding (the U partials sum other rows per group).
+// "onepass_rows" = -1 (default): row groups own interleaved rows (g, g + ngroups, ...) when there are at
+// least 8 groups of at least 128 rows over at least 16 segment blocks -- the groups then read one contiguous
+// window of A instead of ngroups streams R rows apart: configs[1] (16 groups of 512 rows) k_onepass 336.7 ->
+// 331.0 us, the N = 2 and N = 4 strong row shards (4096 / 2048 rows per GPU) 187.8 -> 180.5 and 108.6 ->
+// 106.3 us per iteration -- and consecutive rows otherwise: even or slower at 64-row groups (the N = 8
+// strong shard, 63.0 / 62.7 us on one box, 51.6 -> 52.9 us on another), with one segment block per row
+// (configs[3], 2709 -> 2757 us) and at 2 groups (the weak shard, 328 -> 333.7 us); profiles/r05/layout,
+// profiles/r05/rows.  Results agree to rounding (the U partials sum other rows per group).
 int op_rows_eff(const bpgl_ctx* c) {
     if (c->op_rows >= 0) return c->op_rows;
-    return c->op_SB >= 16 && c->op_ngroups >= 8 && c->op_R >= 512 ? 1 : 0;
+    return c->op_SB >= 16 && c->op_ngroups >= 8 && c->op_R >= 128 ? 1 : 0;
 }
 
 // scratch layout (offsets in bytes)

@@ -275,7 +275,7 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   row group the one-pass kernel reads with cache-allocating loads (launches
  *   alternate the row direction, so the next launch starts on those rows).
  *   "onepass_rows" (default -1 = auto: interleaved when there are at least 8 row
- *   groups of at least 512 rows over at least 16 segment blocks, else 0): 1 = row
+ *   groups of at least 128 rows over at least 16 segment blocks, else 0): 1 = row
  *   group g of the one-pass kernel owns rows g, g + ngroups, ... (the groups read
  *   adjacent rows at once), 0 = R consecutive rows; bpgl_solver_stat("onepass_rows")
  *   reports the form in use.
