@@ -382,7 +382,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     }
     for (; base < nrows + LAG; base += NB) {
 #pragma unroll
-        for (int q = 0; q < NB; ++q) step(NToff{}, q, base + q);
+        for (int q = 0; q < NB; ++q) {
+            // uniform: the last chunk of the ring ends with the drain, not NB-aligned -- leaving here skips
+            // the up to NB - 1 empty steps after it (each still issued its prefetch loads): k_onepass
+            // 330.0 -> 326.0 us at configs[1], 332.7 -> 324.8 us on the weak shard, 53.2 -> 51.7 us on the
+            // N = 8 strong shard, configs[3] unchanged (round 5, profiles/r05/drain_exit)
+            if (base + q >= nrows + LAG) break;
+            step(NToff{}, q, base + q);
+        }
     }
     BPGL_STAMP_AT(2, 1);
     if (failed && lane == 0) atomicOr((unsigned long long*)&p.st->op_fail, 1ull);
