@@ -23,7 +23,6 @@ def main():
     ap.add_argument("--reverse", default="0")
     ap.add_argument("--nt", default="1")
     ap.add_argument("--tails", default="120")
-    ap.add_argument("--fused", default="0")
     ap.add_argument("--colmodes", default="0")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
@@ -36,11 +35,9 @@ def main():
         os.environ["BPGL_TARGET_BLOCKS"] = str(tb)
         gc, b, mu, _ = device_instance(a.m, a.n, 0.4, a.block, TYPE=a.type, seed=1, device=0)
         geo = gc.geometry()
-        for rev, nt, tail, fu, cm in [(int(r), int(n), int(t), int(f), int(c))
-                                      for r in a.reverse.split(",") for n in a.nt.split(",")
-                                      for t in a.tails.split(",") for f in a.fused.split(",")
-                                      for c in a.colmodes.split(",")]:
-            gc.set_tuning("fused", fu)
+        for rev, nt, tail, cm in [(int(r), int(n), int(t), int(c))
+                                  for r in a.reverse.split(",") for n in a.nt.split(",")
+                                  for t in a.tails.split(",") for c in a.colmodes.split(",")]:
             gc.set_tuning("col_mode", cm)
             gc.set_tuning("reverse_rows", rev)
             gc.set_tuning("nt_loads", nt)
@@ -60,7 +57,7 @@ def main():
             gc.solver_step(a.steps // 2)
             kt, _ = gc.kernel_times()
             gc.set_kernel_timing(False)
-            rec = dict(target=tb, reverse=rev, nt=nt, tail=tail, fused=fu, col_mode=cm, geometry=geo,
+            rec = dict(target=tb, reverse=rev, nt=nt, tail=tail, col_mode=cm, geometry=geo,
                        iters_per_s=best,
                        kernel_us={k: round(v * 1e3, 2) for k, v in kt.items()})
             print(json.dumps(rec), flush=True)
