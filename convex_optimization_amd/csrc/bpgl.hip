@@ -204,6 +204,7 @@ int op_cache_eff(const bpgl_ctx* c) {
 // (configs[3], 2709 -> 2757 us) and at 2 groups (the weak shard, 328 -> 333.7 us); profiles/r05/layout,
 // profiles/r05/rows.  Results agree to rounding (the U partials sum other rows per group).
 int op_rows_eff(const bpgl_ctx* c) {
+    if (c->op_gpl == 2) return 0;   // the interleaved kernel is instantiated for SB <= 64 only
     if (c->op_rows >= 0) return c->op_rows;
     return c->op_SB >= 16 && c->op_ngroups >= 8 && c->op_R >= 128 ? 1 : 0;
 }
@@ -331,24 +332,28 @@ Params op_params(const bpgl_ctx* c) {
     q.nparts = c->op_tail_grid;   // shrink partials come from k_onepass_tail
     return q;
 }
-// GPL: granules per lane of the row hand-off (SB <= 64: 1, SB <= 128: 2)
-template <typename T, int GPL>
-const void* onepass_fn_g() { return (const void*)k_onepass<T, OpRing<T>::NB, OpRing<T>::PF, OpLU<T>::LU, GPL>; }
+// GPL: granules per lane of the row hand-off (SB <= 64: 1, SB <= 128: 2); RILV: interleaved row groups
+// (instantiated for GPL 1 only: "onepass_rows" applies when SB <= 64)
+template <typename T, int GPL, bool RILV>
+const void* onepass_fn_g() { return (const void*)k_onepass<T, OpRing<T>::NB, OpRing<T>::PF, OpLU<T>::LU, GPL, RILV>; }
 template <typename T>
-const void* onepass_fn_t(int gpl) { return gpl == 2 ? onepass_fn_g<T, 2>() : onepass_fn_g<T, 1>(); }
-const void* onepass_fn(int dtype, int gpl) {
-    return dtype == BPGL_F32 ? onepass_fn_t<float>(gpl) : dtype == BPGL_F64 ? onepass_fn_t<double>(gpl)
-                                                                             : onepass_fn_t<bf16_t>(gpl);
+const void* onepass_fn_t(int gpl, int rilv) {
+    return gpl == 2 ? onepass_fn_g<T, 2, false>() : rilv ? onepass_fn_g<T, 1, true>() : onepass_fn_g<T, 1, false>();
 }
-template <typename T, int GPL>
+const void* onepass_fn(int dtype, int gpl, int rilv) {
+    return dtype == BPGL_F32 ? onepass_fn_t<float>(gpl, rilv) : dtype == BPGL_F64 ? onepass_fn_t<double>(gpl, rilv)
+                                                                                   : onepass_fn_t<bf16_t>(gpl, rilv);
+}
+template <typename T, int GPL, bool RILV>
 void onepass_launch_g(bpgl_ctx* c) {
-    hipLaunchKernelGGL((k_onepass<T, OpRing<T>::NB, OpRing<T>::PF, OpLU<T>::LU, GPL>),
+    hipLaunchKernelGGL((k_onepass<T, OpRing<T>::NB, OpRing<T>::PF, OpLU<T>::LU, GPL, RILV>),
                        dim3((unsigned)(c->op_ngroups * c->op_SB)), dim3(kThreads), 0, c->stream, op_params(c), c->op);
 }
 template <typename T>
 void onepass_launch_t(bpgl_ctx* c) {
-    if (c->op_gpl == 2) onepass_launch_g<T, 2>(c);
-    else onepass_launch_g<T, 1>(c);
+    if (c->op_gpl == 2) onepass_launch_g<T, 2, false>(c);
+    else if (c->op.rilv) onepass_launch_g<T, 1, true>(c);
+    else onepass_launch_g<T, 1, false>(c);
 }
 int onepass_launch(bpgl_ctx* c) {
     switch (c->dtype) {
@@ -418,7 +423,7 @@ const char* onepass_ineligible(bpgl_ctx* c) {
     if (!c->rows && (c->nranks != 1 || c->comm || c->external))
         return "column shards need a single rank without a communicator (row shards run it on several)";
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_gpl), kThreads, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_gpl, op_rows_eff(c)), kThreads, 0) != hipSuccess || nb < 1)
         return "kernel does not fit on a CU";
     if ((int64_t)c->op_ngroups * c->op_SB > (int64_t)nb * c->cus) return "grid exceeds the resident capacity";
     return nullptr;

@@ -74,7 +74,8 @@ struct OnePassArgs {
     long long fail_at;           // test hook: iteration whose launch reports a hand-off failure (-1: none)
     int rowb;                    // k_onepass_tail: blocks appended after the column blocks that only run
                                  // the residual update (0: the column blocks run it first, as before)
-    int rilv;                    // 1: row group g owns rows g, g + ngroups, ... (interleaved), 0: R consecutive rows
+    int rilv;                    // 1: row group g owns rows g, g + ngroups, ... (interleaved; the k_onepass<..., true>
+                                 // instantiation), 0: R consecutive rows
     int tailw;                   // k_onepass_tail, one rank: every lane sums its column's U partials itself
                                  // (wave-owned 64-column tiles, no LDS fold; ngroups <= kOpTailWaveGroups)
 };
@@ -200,7 +201,7 @@ struct OnePassGeo {
     static constexpr int BC = kWaves * WC;   // columns per segment block
 };
 
-template <typename T, int NB, int PF, int LU, int GPL>
+template <typename T, int NB, int PF, int LU, int GPL, bool RILV>
 __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o) {
     if (p.st->done) return;
     using G = OnePassGeo<LU, T>;
@@ -218,11 +219,16 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
     else { grp = b / SB; sb = b % SB; }
     // this group's rows: R consecutive ones, or (rilv) rows grp, grp + ngroups, ... -- the groups then
     // read adjacent rows at once (one contiguous window of A instead of ngroups streams R rows apart)
-    const long long gs = o.rilv ? o.ngroups : 1;
-    const long long i0 = o.rilv ? grp : (long long)grp * o.R;
+    // (a compile-time choice: the runtime stride cost the consecutive form 0.4-0.8 % -- the row step is
+    // sensitive to every scalar instruction at one wave per SIMD; profiles/r05/consec)
+    // (the interleaved instantiation keeps the runtime form of these expressions: written with the
+    // compile-time stride it measured 0.6 % slower at configs[1])
+    const bool ilv = RILV && o.rilv;
+    const long long gs = ilv ? o.ngroups : 1;
+    const long long i0 = ilv ? grp : (long long)grp * o.R;
     const long long i1 = i0 + o.R < p.m ? i0 + o.R : p.m;
-    const int nrows = o.rilv ? (grp < p.m ? (int)((p.m - grp + gs - 1) / gs) : 0) : (i1 > i0 ? (int)(i1 - i0) : 0);
-    auto rowat = [&](long long i) -> long long { return i0 + i * gs; };   // this group's i-th row
+    const int nrows = ilv ? (grp < p.m ? (int)((p.m - grp + gs - 1) / gs) : 0) : (i1 > i0 ? (int)(i1 - i0) : 0);
+    auto rowat = [&](long long i) -> long long { return RILV ? i0 + i * gs : i0 + i; };   // this group's i-th row
     // launches alternate the row direction; each reads the last cache_permille of its rows with
     // cache-allocating loads, which the next launch (opposite direction) reads first from the
     // Infinity Cache (only the small tail kernel runs in between)

@@ -277,8 +277,8 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   "onepass_rows" (default -1 = auto: interleaved when there are at least 8 row
  *   groups of at least 128 rows over at least 16 segment blocks, else 0): 1 = row
  *   group g of the one-pass kernel owns rows g, g + ngroups, ... (the groups read
- *   adjacent rows at once), 0 = R consecutive rows; bpgl_solver_stat("onepass_rows")
- *   reports the form in use.
+ *   adjacent rows at once; with at most 64 segment blocks per row, else always 0),
+ *   0 = R consecutive rows; bpgl_solver_stat("onepass_rows") reports the form in use.
  *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for
