@@ -35,8 +35,10 @@ across column shards, it is the reference's two passes (A^T r, then A D).
           right-hand sides on bf16 A), one GPU.
 
 Timing (every workload): W untimed warm-up iterations; an eager window of
-max(K, 512) iterations with HIP events around every kernel on the solver stream
-(the per-kernel averages behind `roofline`, and the clock ramp of a fresh box);
+max(K, 512) iterations (side legs: max(K, 128)) with HIP events around every kernel
+on the solver stream (the per-kernel averages behind `roofline`, and the clock ramp
+of a fresh box), lengthened on a one-pass leg until it contains an exact-gradient
+refresh (a one-pass leg that timed none fails);
 then `--windows` (default 5) windows of exactly K graph-replayed iterations, each
 bracketed by a barrier and device synchronisation, max over ranks.  value and
 ms_per_step come from the median window, with the one-pass exact-gradient refresh
@@ -325,6 +327,18 @@ def median(v):
     return v[k // 2] if k % 2 else 0.5 * (v[k // 2 - 1] + v[k // 2])
 
 
+def eager_window_len(steps, ramp, warmup, period, onepass):
+    """iterations of the eager window: max(K, ramp), lengthened on a one-pass leg so that it
+    contains an exact-gradient refresh (the refresh runs before iteration t when t is a positive
+    multiple of `period`; the window covers iterations [warmup, warmup + n)), whose event-timed
+    cost is folded into every window's rate"""
+    n = max(steps, ramp)
+    if onepass and period > 0:
+        first = max(period, -(-warmup // period) * period)
+        n = max(n, first - warmup + 1)
+    return n
+
+
 def measure(ctx, args, m, n_total):
     """W warm-up iterations, an eager window with per-kernel HIP events (max(K, 512) iterations),
     then `windows` graph windows of exactly K iterations (see the module docstring).  A window is
@@ -356,8 +370,9 @@ def measure(ctx, args, m, n_total):
         op0 = gc.solver_stat("onepass")
         gc.solver_step(args.warmup)
         sync()
-        # eager window: kernel averages (events on the solver stream) + clock ramp
-        n_ev = max(args.steps, args.ramp)
+        # eager window: kernel averages (events on the solver stream) + clock ramp, and on a
+        # one-pass leg at least one exact-gradient refresh
+        n_ev = eager_window_len(args.steps, args.ramp, args.warmup, gc.solver_stat("refresh_period"), op0)
         progress(f"  eager window of {n_ev} iterations with kernel events")
         gc.set_kernel_timing(True)
         r0 = gc.solver_stat("refreshes")
@@ -370,6 +385,10 @@ def measure(ctx, args, m, n_total):
         st = gc.solver_status()   # completes any iteration a failed one-pass launch lost (outside the windows)
         eager_op = int(min(ctx.gather(gc.solver_stat("onepass"))))
         period = gc.solver_stat("refresh_period")
+        if eager_op and period and not refresh_ms > 0.0:
+            raise MeasureError(f"one-pass leg timed no exact-gradient refresh in its eager window "
+                               f"({n_ev} iterations from {args.warmup}, period {period}): its rate would leave "
+                               f"the refresh out")
         # graph windows; after each, the status call (outside the window) re-runs iterations a
         # failed one-pass launch lost -- such a window did not do its K iterations, and a window
         # after a fallback runs the two-pass kernels: neither counts toward the median

@@ -45,28 +45,6 @@ constexpr int kMaxRanks = 64;
 
 int vec_elems(int dtype) { return dtype == BPGL_F32 ? 4 : dtype == BPGL_F64 ? 2 : 8; }
 
-constexpr int kMaskWords = 32;   // CU mask words queried (1024 CUs)
-
-int popcount_mask(const uint32_t* mask, int words, int cus) {
-    int n = 0;
-    for (int i = 0; i < words; ++i) {
-        uint32_t v = mask[i];
-        if (32 * i >= cus) break;
-        if (32 * (i + 1) > cus) v &= (1u << (cus - 32 * i)) - 1u;
-        n += __builtin_popcount(v);
-    }
-    return n;
-}
-
-// CUs a stream may use (its CU mask, hipExtStreamGetCUMask), 0 if unknown
-int stream_cus(hipStream_t s, int dev_cus) {
-    uint32_t mask[kMaskWords] = {};
-    if (hipExtStreamGetCUMask(s, kMaskWords, mask) != hipSuccess) {
-        (void)hipGetLastError();   // not sticky: later launch checks read hipGetLastError
-        return 0;
-    }
-    return popcount_mask(mask, kMaskWords, dev_cus);
-}
 }  // namespace
 
 struct bpgl_ctx {

@@ -32,6 +32,40 @@ constexpr int kGraphIters = 8;   // iterations captured per replayed hipGraph (p
 // costs about log2(n) replays instead of n / 8
 constexpr int kGraphLevels = 7;
 constexpr int kGraphMaxIters = 1 << (kGraphLevels - 1);
+
+constexpr int kMaskWords = 32;   // CU mask words queried (1024 CUs)
+
+inline int popcount_mask(const uint32_t* mask, int words, int cus) {
+    int n = 0;
+    for (int i = 0; i < words; ++i) {
+        uint32_t v = mask[i];
+        if (32 * i >= cus) break;
+        if (32 * (i + 1) > cus) v &= (1u << (cus - 32 * i)) - 1u;
+        n += __builtin_popcount(v);
+    }
+    return n;
+}
+
+// CUs a stream may use (its CU mask, hipExtStreamGetCUMask), 0 if unknown
+inline int stream_cus(hipStream_t s, int dev_cus) {
+    uint32_t mask[kMaskWords] = {};
+    if (hipExtStreamGetCUMask(s, kMaskWords, mask) != hipSuccess) {
+        (void)hipGetLastError();   // the query's own error only: not sticky, later launch checks read it
+        return 0;
+    }
+    return popcount_mask(mask, kMaskWords, dev_cus);
+}
+
+// CUs a kernel launched on stream s can occupy: the stream's CU mask when it has one, else the device's
+inline int usable_cus(hipStream_t s, int device) {
+    int dev = 0;
+    if (hipDeviceGetAttribute(&dev, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || dev <= 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const int n = stream_cus(s, dev);
+    return (n > 0 && n < dev) ? n : dev;
+}
 }  // namespace bpgl_host
 
 #define HIP_TRY(expr)                                                                        \

@@ -41,6 +41,7 @@ struct bpgl_panel {
     hipGraphExec_t gexec_ref = nullptr;   // carry_g: a graph whose first iteration is the exact-gradient one
     int fuse_update = 1;          // one block, x deferred: reduce + line search + R update in one launch ("fuse_update")
     int fuse_ok = 0;              // ... and the shape and occupancy admit it (panel_fused_geo, set at bind)
+    int fuse_cus = 0;             // the CUs that check counted (the stream's CU mask, or the device)
     int fuse_grid = 1024;         // its grid: at most this many blocks, k x G ("fuse_grid": 256, 512 or 1024;
                                   // 1024 measured best with 512, +0.4 % over 256: profiles/r05/panel_fused)
     int64_t t_host = 0;           // iterations enqueued since the last reset
@@ -183,16 +184,19 @@ int panel_reduce_upd(bpgl_panel* c, int cflag) {
     LAUNCH_CHECK("k_panel_reduce_upd");
     return 0;
 }
-// the fused reduce + update needs its k x G blocks resident together
+// the fused reduce + update needs its k x G blocks resident together: on the CUs the stream may use
+// (a CU-masked stream from bpgl_stream_create gets fewer), else the two-kernel form runs
 void panel_fuse_check(bpgl_panel* c) {
-    int G = 0, U = 0, nb = 0, cus = 0;
+    int G = 0, U = 0, nb = 0;
     c->fuse_ok = 0;
-    if (panel_fused_geo(c, &G, &U) &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, panel_fused_fn(U), kThreads, 0) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess &&
-        (int64_t)nb * cus >= (int64_t)c->k * G)
-        c->fuse_ok = 1;
-    (void)hipGetLastError();
+    c->fuse_cus = 0;
+    if (!panel_fused_geo(c, &G, &U)) return;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, panel_fused_fn(U), kThreads, 0) != hipSuccess) {
+        (void)hipGetLastError();   // the query's own error only
+        return;
+    }
+    c->fuse_cus = usable_cus(c->stream, c->device);
+    if ((int64_t)nb * c->fuse_cus >= (int64_t)c->k * G) c->fuse_ok = 1;
 }
 int panel_reduce(bpgl_panel* c, double* out, int mode) {
     hipLaunchKernelGGL(k_panel_reduce, dim3((unsigned)(c->k * cdiv(c->m, kLspRows))), dim3(kThreads), 0, c->stream,
@@ -626,6 +630,7 @@ int bpgl_panel_stat(const bpgl_panel* c, const char* key, int64_t* value) {
     if (!c || !key || !value) return fail(BPGL_E_ARG, "null argument");
     if (!strcmp(key, "iters_enqueued")) *value = c->t_host;
     else if (!strcmp(key, "exact_gradients")) *value = c->n_exact;
+    else if (!strcmp(key, "fuse_cus")) *value = c->fuse_cus;   // CUs the fused-update check counted
     else return fail(BPGL_E_ARG, "unknown panel stat '%s'", key);
     return 0;
 }

@@ -76,7 +76,10 @@ class PanelLasso:
 
     KERNEL_KINDS = ("pass1_mfma", "pass2_mfma", "reduce", "step", "update")
 
-    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0):
+    def __init__(self, A, Block=1, nrhs=128, device=None, kchunks=0, cu_mask=None, lda=None):
+        """cu_mask: CU mask words (bit i = CU i) -> the solver runs on a CU-masked stream of its own
+        (bpgl_stream_create; the fused reduce + update is admitted only if it fits those CUs).
+        lda: row stride of the stored bf16 A (>= n, a multiple of 8; default n), the padding zeroed."""
         L = _lib()
         self.Block = int(Block)
         self.nrhs = int(nrhs)
@@ -88,16 +91,27 @@ class PanelLasso:
             device = A.device if isinstance(A, torch.Tensor) and A.is_cuda else torch.cuda.current_device()
         self.device = torch.device("cuda", torch.device(device).index if not isinstance(device, int) else device)
         torch.cuda.set_device(self.device)
-        self.stream = torch.cuda.Stream(device=self.device)
+        if cu_mask is not None:
+            from .gpu_calculation import _masked_stream
+            self.stream = _masked_stream(self.device, list(cu_mask))
+        else:
+            self.stream = torch.cuda.Stream(device=self.device)
         ctx = ctypes.c_void_p()
         N.check(L.bpgl_panel_create(ctypes.byref(ctx), self.device.index, H, K, self.Block, self.nrhs,
                                     int(kchunks), ctypes.c_void_p(self.stream.cuda_stream)), "bpgl_panel_create")
         self._ctx = ctx
-        lda = K
+        lda = K if lda is None else int(lda)
+        self.lda = lda
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             A_src = A if isinstance(A, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(A))
-            self._A = A_src.to(device=self.device, dtype=torch.bfloat16).contiguous()     # [m][n]
+            A_src = A_src.to(device=self.device, dtype=torch.bfloat16)
+            if lda == K:
+                self._A = A_src.contiguous()                                                # [m][n]
+            else:                                                                           # [m][lda]
+                self._A_store = torch.zeros(H, lda, dtype=torch.bfloat16, device=self.device)
+                self._A_store[:, :K] = A_src
+                self._A = self._A_store[:, :K]
             nbytes = int(L.bpgl_panel_scratch_bytes(ctx))
             self._scratch = torch.empty(nbytes // 8 + 64, dtype=torch.float64, device=self.device)
             base = (self._scratch.data_ptr() + 255) // 256 * 256
@@ -129,8 +143,10 @@ class PanelLasso:
 
     @property
     def A_bf16(self):
-        """The stored A (m x n, bf16) -- the matrix the problems are defined by."""
-        return self._A
+        """A copy of the stored A (m x n, bf16) -- the matrix the problems are defined by.  A copy:
+        bind took the passes' tiled images of A (include/bpgl.h), so writing into the stored A
+        would change bpgl_panel_diag's input but not the solver's."""
+        return self._A.clone()
 
     @property
     def diag_ATA(self):

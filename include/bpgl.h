@@ -313,8 +313,13 @@ int bpgl_panel_create(bpgl_panel** out, int device, int64_t m, int64_t n, int32_
                       int32_t kchunks /* <= 0: automatic */, void* hip_stream);
 void bpgl_panel_destroy(bpgl_panel* ctx);
 int64_t bpgl_panel_scratch_bytes(const bpgl_panel* ctx);
-/* bind makes the passes' tiled copies of A inside the scratch (two more m x n bf16 images: each pass's
- * 64-deep stage is then one contiguous 32 KiB); A itself must stay valid while the context is bound. */
+/* bind COPIES A's contents into two tiled m x n bf16 images inside the scratch (one per pass: each pass's
+ * 64-deep stage is then one contiguous 32 KiB), so bpgl_panel_scratch_bytes includes 4 m n bytes for
+ * them on top of the vectors.  The solver passes and bpgl_panel_mtm / _mm read those copies; only
+ * bpgl_panel_diag reads A itself.  A must stay valid while the context is bound, and after A's
+ * contents change the context must be bound again (the copies are not refreshed).  The fused
+ * reduce + update form ("fuse_update" below) is admitted at bind only if its blocks fit on the CUs
+ * the context's stream may use (a CU-masked stream counts its own CUs; stat "fuse_cus"). */
 int bpgl_panel_bind(bpgl_panel* ctx, const void* A /* [m][lda] bf16 */, int64_t lda, void* scratch,
                     int64_t scratch_bytes);
 int bpgl_panel_diag(bpgl_panel* ctx, double* out /* nullable, n fp64 */);
@@ -350,7 +355,7 @@ int bpgl_panel_kernel_times(bpgl_panel* ctx, double* avg_ms /* 5: pass1, pass2, 
  * 1024 -- get_tuning reports the form in effect; a reset must follow a change): the split-K reduce, each
  * RHS's line search and R += gamma S run as ONE launch whose blocks wait for their RHS's step size
  * (bitwise the two-kernel result); it needs its blocks co-resident, which bpgl_panel_bind checks with
- * the occupancy API -- should a wait still run out (another kernel holding CUs), nothing is updated and
+ * the occupancy API against the stream's usable CUs (its CU mask, else the device) -- should a wait still run out (another kernel holding CUs), nothing is updated and
  * bpgl_panel_status returns BPGL_E_EXCHANGE.  "fuse_grid" (256 / 512 / 1024, default 1024): its grid.
  * "defer_x" (0 / 1; default 1, one feature block; a reset must follow a change): the
  * update x += gamma D' of an iteration is applied by the next pass-1 epilogue (and at

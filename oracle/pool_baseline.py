@@ -73,7 +73,9 @@ def run_pool(A, b, mu, BLOCK, P, iters):
             Ax[k] += gamma * s23                                          # :155
         el = time.perf_counter() - t1
     finally:
-        pool.terminate()
+        # close + join, not terminate: the workers exit on their own once the task queue drains,
+        # so no SIGTERM stack traces land in the logs of a profiled bench run
+        pool.close()
         pool.join()
     return x_block.reshape(-1), el, t1 - t0
 

@@ -23,7 +23,8 @@ A is NOT stored: it is regenerated bit-exactly by
 ``np.random.seed(seed)`` in parameters.py:17-21); every fixture stores a
 checksum of A so a regeneration mismatch is detected.
 
-Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [CASE ...]   (writes tests/golden/*.npz; all cases
+        when none is named, else only the named ones and, if asked for, "kats")
 """
 import os
 import random
@@ -159,23 +160,45 @@ def make_kats(mods):
     print("kats: written")
 
 
+# the one-pass stop rule (BLOCK = 1): the device path carries g += gamma A^T (A D) between exact
+# refreshes of A^T r every 256 iterations, and evaluates error_crit (cpu_calculation.py:15-20) on
+# the carried g.  These cases make the reference's ClassLassoCPU stop (lasso.py:141-150) where the
+# carried g is oldest (t = 511: 255 iterations since the refresh at 256) and right after a refresh
+# (t = 257, t = 513).  Instance 256 x 4096: it converges slowly enough that at t ~ 500 the error
+# criterion is still 4e-5 and its P = 1 / P = 4 summation orders agree to 6e-8 relative, while
+# each bound sits >= 0.5 % inside the gap between the stopping error and the running minimum
+# before it (the bounds were read off the C oracle's err trace of the same instance).
+STOP_CASES = {
+    "stop511_b1_p1_f32in": (1, 3.91e-5),
+    "stop257_b1_p4_f32in": (4, 1.92e-4),
+    "stop513_b1_p4_f32in": (4, 3.867e-5),
+}
+
+
 def main():
+    want = set(sys.argv[1:])
     mods = _import_reference()
-    make_kats(mods)
+
+    def case(name, *a, **k):
+        if not want or name in want:
+            make_case(mods, name, *a, **k)
+
+    if not want or "kats" in want:
+        make_kats(mods)
     # config 1 (BASELINE.json configs[0]): m=512 n=2048 fp64, 200 iterations
-    make_case(mods, "c1_b1_p1_f64", 20190325, 512, 2048, 0.4, 1, 1, 200, False)
-    make_case(mods, "c1_b2_p4_f64", 20190325, 512, 2048, 0.4, 2, 4, 200, False)
+    case("c1_b1_p1_f64", 20190325, 512, 2048, 0.4, 1, 1, 200, False)
+    case("c1_b2_p4_f64", 20190325, 512, 2048, 0.4, 2, 4, 200, False)
     # fp32-rounded inputs (GPU fp32 storage parity)
-    make_case(mods, "c1_b1_p1_f32in", 20190326, 512, 2048, 0.4, 1, 1, 200, True)
-    make_case(mods, "c1_b2_p4_f32in", 20190326, 512, 2048, 0.4, 2, 4, 200, True)
+    case("c1_b1_p1_f32in", 20190326, 512, 2048, 0.4, 1, 1, 200, True)
+    case("c1_b2_p4_f32in", 20190326, 512, 2048, 0.4, 2, 4, 200, True)
     # ragged / odd shapes: rows not a multiple of anything, narrow blocks
-    make_case(mods, "ragged_b3_p2_f32in", 4242, 77, 120, 0.4, 3, 2, 60, True)
+    case("ragged_b3_p2_f32in", 4242, 77, 120, 0.4, 3, 2, 60, True)
     # ERR_BOUND stopping (lasso.py:141-150)
-    make_case(mods, "bound_b4_p2_f32in", 99, 96, 320, 0.3, 4, 2, 2000, True,
-              err_bound=1e-3)
+    case("bound_b4_p2_f32in", 99, 96, 320, 0.3, 4, 2, 2000, True, err_bound=1e-3)
+    for name, (P, eb) in STOP_CASES.items():
+        case(name, 20190327, 256, 4096, 0.4, 1, P, 600, True, err_bound=eb)
     # random block order (lasso.py:303-306), seeded stdlib random
-    make_case(mods, "random_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 64, True,
-              random_order=True, py_seed=5)
+    case("random_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 64, True, random_order=True, py_seed=5)
 
 
 if __name__ == "__main__":

@@ -72,6 +72,38 @@ def test_reference_fixture(golden, case, type_name):
     np.testing.assert_allclose(one["err_iter"][:T], fx["err_iter"][:T], rtol=1e-6, atol=1e-9)
 
 
+STOP_CASES = ["stop511_b1_p1_f32in", "stop257_b1_p4_f32in", "stop513_b1_p4_f32in"]
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+@pytest.mark.parametrize("type_name", ["float", "double"])
+@pytest.mark.parametrize("case", STOP_CASES)
+def test_stop_rule_pinned_to_reference(golden, case, type_name, use_graph):
+    """ERR_BOUND on the default one-pass path (lasso.py:141-150, cpu_calculation.py:15-20).  The
+    error criterion is evaluated on the carried g (g += gamma A^T (A D), exact A^T r every 256
+    iterations); the reference's ClassLassoCPU evaluates it on the exact A^T r.  The fixtures stop
+    where the carried g is oldest (t = 511) and right after a refresh (t = 257, 513): the stop
+    iteration and the stopped flag must be the reference's exactly, x within 1e-9 and the
+    err_iter trace within 1e-6 relative, with the one-pass kernel in use throughout."""
+    fx = golden(case)
+    A = oracle.fixture_A(fx)
+    gc = make_cls(type_name)(A, 1, device=0)
+    assert used_onepass(gc, fx["b"], float(fx["mu"]))
+    res = gc.run(fx["b"], float(fx["mu"]), int(fx["ITER_MAX"]), err_bound=float(fx["err_bound"]),
+                 record=True, use_graph=use_graph)
+    assert gc.solver_stat("onepass") == 1 and gc.solver_stat("fallbacks") == 0
+    T = int(fx["t_last"])
+    assert bool(fx["stopped"]) and res["stopped"]
+    assert res["t_last"] == T, (res["t_last"], T)
+    assert rel(res["x"], fx["x"]) <= 1e-9, rel(res["x"], fx["x"])
+    np.testing.assert_allclose(res["err_iter"][:T + 1], fx["err_iter"][:T + 1], rtol=1e-6)
+    # the margin the carried g had: how far the stopping error sits below the bound, and the
+    # smallest error before it above the bound
+    eb = float(fx["err_bound"])
+    print(f"{case} {type_name} graph={use_graph}: stop t={T}, err[T]/bound={res['err_iter'][T] / eb:.6f}, "
+          f"min err[:T]/bound={res['err_iter'][:T].min() / eb:.6f}")
+
+
 # (m, n, dtype): ragged widths (not a multiple of the 4096-column segment block), fewer
 # rows than row groups, many row groups, 64 segment blocks per row, tiny problems
 SHAPES = [(1000, 4100, "float"), (37, 9000, "float"), (4099, 1536, "float"), (256, 262144, "float"),

@@ -397,3 +397,41 @@ def test_panel_fused_reduce_update_eligibility():
     assert pl.get_tuning("fuse_update") == 0
     with pytest.raises(Exception):
         pl.set_tuning("fuse_update", 2)
+
+
+def test_panel_fused_update_honours_the_stream_cu_mask():
+    """k_panel_reduce_upd needs its k x G blocks co-resident.  On a CU-masked stream
+    (bpgl_stream_create, here 1/8 of the CUs) the check at bind counts the stream's CUs, finds that
+    the 1024 blocks of configs[4]'s geometry (m = 8192, k = 128) do not fit, and the two-kernel form
+    runs -- bitwise the fused result of the unmasked context."""
+    from convex_optimization_amd.distributed import xcd_symmetric_cu_mask
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    Ab, B, mu = instance(8192, 1024, 128, seed=31)
+    full = PanelLasso(Ab, 1, nrhs=128, device=0)
+    assert full.get_tuning("fuse_update") == 1 and full.stat("fuse_cus") == cus
+    masked = PanelLasso(Ab, 1, nrhs=128, device=0, cu_mask=xcd_symmetric_cu_mask(0, 8, cus))
+    assert masked.stat("fuse_cus") == cus // 8
+    assert masked.get_tuning("fuse_update") == 0
+    a = full.run(B, mu, 24, record=True)
+    b = masked.run(B, mu, 24, record=True)
+    assert a["iters"] == b["iters"] == 24
+    np.testing.assert_array_equal(a["x"], b["x"])
+    np.testing.assert_array_equal(a["err_iter"], b["err_iter"])
+
+
+def test_panel_padded_lda_is_bitwise():
+    """a row-padded A (lda = n + 64; the C ABI accepts any lda >= n that is a multiple of
+    8) gives bitwise the iterates, products and column norms of the lda = n binding"""
+    Ab, B, mu = instance(512, 2048, 32, seed=41)
+    pl0 = PanelLasso(Ab, 2, nrhs=32, device=0)
+    pl1 = PanelLasso(Ab, 2, nrhs=32, device=0, lda=2048 + 64)
+    assert pl1.lda == 2048 + 64
+    np.testing.assert_array_equal(pl0.diag_ATA, pl1.diag_ATA)
+    rs = np.random.RandomState(2)
+    R, D = rs.randn(512, 32), rs.randn(1024, 32)
+    for blk in (0, 1):
+        np.testing.assert_array_equal(pl0.mat_tMulMat(R, blk).cpu().numpy(), pl1.mat_tMulMat(R, blk).cpu().numpy())
+        np.testing.assert_array_equal(pl0.matMulMat(D, blk).cpu().numpy(), pl1.matMulMat(D, blk).cpu().numpy())
+    np.testing.assert_array_equal(pl0.run(B, mu, 30)["x"], pl1.run(B, mu, 30)["x"])
+    one0, one1 = PanelLasso(Ab, 1, nrhs=32, device=0), PanelLasso(Ab, 1, nrhs=32, device=0, lda=2048 + 64)
+    np.testing.assert_array_equal(one0.run(B, mu, 30)["x"], one1.run(B, mu, 30)["x"])

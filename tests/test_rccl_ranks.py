@@ -110,6 +110,25 @@ def test_rccl_row_shards_onepass_cu_masked(golden, world, tmp_path):
     np.testing.assert_array_equal(out[0]["x_graph"], out[0]["x_eager"])
 
 
+@pytest.mark.parametrize("case,world", [("stop511_b1_p1_f32in", 2), ("stop257_b1_p4_f32in", 4),
+                                        ("stop513_b1_p4_f32in", 2)])
+def test_rccl_row_shards_stop_rule_pinned(golden, case, world, tmp_path):
+    """ERR_BOUND on one-pass row shards over RCCL (each rank on its own CUs): the error criterion
+    comes from the all-reduced carried g, and the stop iteration must be the reference's own
+    (ClassLassoCPU, lasso.py:141-150) on every rank, in graph replay and eager, with no fallback."""
+    fx = golden(case)
+    out = _launch(case, "rows", tmp_path, world, ["--cumask"])
+    T = int(fx["t_last"])
+    for tag in ("graph", "eager"):
+        for o in out:
+            assert int(o[f"onepass_{tag}"]) == 1 and int(o[f"fallbacks_{tag}"]) == 0
+            assert int(o[f"t_last_{tag}"]) == T and bool(o[f"stopped_{tag}"]), (tag, int(o[f"t_last_{tag}"]), T)
+        for o in out[1:]:
+            np.testing.assert_array_equal(out[0][f"x_{tag}"], o[f"x_{tag}"])
+        assert rel(out[0][f"x_{tag}"], fx["x"]) <= 1e-9, (tag, rel(out[0][f"x_{tag}"], fx["x"]))
+        np.testing.assert_allclose(out[0][f"err_{tag}"][:T + 1], fx["err_iter"][:T + 1], rtol=1e-6)
+
+
 def test_rccl_row_shards_collective_recovery(golden, tmp_path):
     """One rank's one-pass launch fails (test hook on rank 0 only, inside an 8-iteration graph):
     its flag rides the all-reduce, every rank skips the same iterations, and every rank's
