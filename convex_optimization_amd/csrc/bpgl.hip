@@ -141,10 +141,15 @@ void geometry(bpgl_ctx* c) {
     const int bc = c->dtype == BPGL_F32 ? OnePassGeo<4, float>::BC
                  : c->dtype == BPGL_F64 ? OnePassGeo<4, double>::BC : OnePassGeo<3, bf16_t>::BC;
     const int64_t SB = cdiv(c->wp, bc);
-    c->op_shape = c->nblock == 1 && SB <= kOpMaxSB && SB <= c->cus;
+    // op_shape: the one-pass buffers and geometry exist (one block, SB <= 128).  Whether the persistent
+    // grid fits the CUs (ngroups x SB co-resident blocks) is onepass_ineligible's question: with more
+    // segment blocks than CUs (a row of 524288 fp32 columns on a 64- or 32-CU partition) there is one
+    // row group, the one-pass iteration is ineligible, and RCCL row shards run the two-pass row
+    // iteration on these buffers
+    c->op_shape = c->nblock == 1 && SB <= kOpMaxSB;
     c->op_gpl = SB > 64 ? 2 : 1;   // k_onepass<..., 2> relies on SB > 64
     if (c->op_shape) {
-        int64_t ng = std::min<int64_t>(std::min<int64_t>(c->cus / SB, c->m), kOpMaxGroups);
+        int64_t ng = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(c->cus / SB, c->m), kOpMaxGroups));
         const int64_t R = cdiv(c->m, ng);
         ng = cdiv(c->m, R);
         c->op_SB = (int)SB;

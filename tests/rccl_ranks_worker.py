@@ -6,7 +6,7 @@ hosts and moves the all-reduce over loopback sockets (the same trick as tools/re
 The data path is the product's: libbpgl's communicator, the all-reduce issued on the solver
 stream.
 
-usage: rccl_ranks_worker.py CASE SHARD OUTDIR [--cumask] [--fail-rank R --fail-at T]
+usage: rccl_ranks_worker.py CASE SHARD OUTDIR [--cumask] [--fail-rank R --fail-at T] [--iters N]
   CASE: a reference fixture of tests/golden, or longrun_<config> (a full-size long-horizon fixture,
         row shards only: see longrun())
   SHARD: columns | rows
@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--cumask", action="store_true")
     ap.add_argument("--fail-rank", type=int, default=-1)
     ap.add_argument("--fail-at", type=int, default=-1)
+    ap.add_argument("--iters", type=int, default=0, help="longrun: iterations (0: the fixture's own)")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ["NCCL_HOSTID"] = f"bpgl-test-rank{rank}"   # before the communicator is created
@@ -104,6 +105,7 @@ def longrun(a, fx, rank, world, np, torch, dist, D, GPU_Calculation):
     import hash_instance as H
 
     m, n, iters, mu = int(fx["m"]), int(fx["n"]), int(fx["iters"]), float(fx["mu"])
+    iters = a.iters or iters
     s, e = D.row_bounds(m, rank, world)
     A = H.torch_A(e - s, n, "cuda:0", row0=s)
     rows, cols = fx["A_rows"], fx["A_cols"]

@@ -135,11 +135,13 @@ def test_gauss_instance_is_deterministic_and_gaussian():
     assert not np.array_equal(A1, oracle.gauss_instance(8, 512, 1024)[0])
 
 
-def test_gauss_fixture_samples_match_the_generator():
-    """tests/golden/gauss_configs3.npz (configs[3] at full size, C oracle, tests/golden/make_gauss.py)
-    was made from this generator: its stored A samples of 64 rows are regenerated bit for bit"""
+@pytest.mark.parametrize("name", ["gauss_configs3", "gauss_configs2"])
+def test_gauss_fixture_samples_match_the_generator(name):
+    """tests/golden/gauss_configs{3,2}.npz (configs[3] / configs[2] at full size, C oracle,
+    tests/golden/make_gauss.py) were made from this generator: their stored A samples of 64 rows are
+    regenerated bit for bit"""
     import os
-    path = os.path.join(os.path.dirname(__file__), "golden", "gauss_configs3.npz")
+    path = os.path.join(os.path.dirname(__file__), "golden", name + ".npz")
     fx = dict(np.load(path))
     n, seed = int(fx["n"]), int(fx["seed"])
     for r, c, v in list(zip(fx["A_rows"], fx["A_cols"], fx["A_samples"]))[:64]:
