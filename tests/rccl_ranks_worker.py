@@ -7,6 +7,7 @@ The data path is the product's: libbpgl's communicator, the all-reduce issued on
 stream.
 
 usage: rccl_ranks_worker.py CASE SHARD OUTDIR [--cumask] [--fail-rank R --fail-at T] [--iters N]
+                           [--exchange-fp32]
   CASE: a reference fixture of tests/golden, or longrun_<config> (a full-size long-horizon fixture,
         row shards only: see longrun())
   SHARD: columns | rows
@@ -34,6 +35,7 @@ def main():
     ap.add_argument("--fail-rank", type=int, default=-1)
     ap.add_argument("--fail-at", type=int, default=-1)
     ap.add_argument("--iters", type=int, default=0, help="longrun: iterations (0: the fixture's own)")
+    ap.add_argument("--exchange-fp32", action="store_true", help="longrun: the opt-in fp32 exchange (tuning -1)")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ["NCCL_HOSTID"] = f"bpgl-test-rank{rank}"   # before the communicator is created
@@ -120,6 +122,8 @@ def longrun(a, fx, rank, world, np, torch, dist, D, GPU_Calculation):
     mask = D.xcd_symmetric_cu_mask(rank, world, torch.cuda.get_device_properties(0).multi_processor_count) \
         if a.cumask else None
     gc = GC(A, 1, device=0, comm=D.RankComm(rank, world), shard="rows", cu_mask=mask)
+    if a.exchange_fp32:
+        gc.set_tuning("exchange_fp32", -1)
     torch.cuda.synchronize()
     dist.barrier()
     res = gc.run(b, mu, iters, record=True, use_graph=True)

@@ -62,6 +62,52 @@ def test_long_horizon_against_oracle(name):
     np.testing.assert_allclose(res["err_iter"][:IT], ref, rtol=1e-4, atol=1e-6 * ref[0])
 
 
+def stop_target(err, lo=257, hi=320, gap=1.02):
+    """(t, bound): the iteration t in [lo, hi] (just past the first exact refresh) at which the error
+    criterion trace first falls below `bound`, bound at the geometric mean of err[t] and the smallest
+    error before t; of the candidates whose two errors are at least `gap` apart, the one with the
+    widest margin.  Not later in the solve: near convergence the criterion -- a max over coordinates
+    of differences of nearly equal numbers -- moves by several per cent between any two summation
+    orders (the reference's own P = 1 and P = 4 runs of one instance differ by 84 % at err ~ 4e-8;
+    the device's trace and the oracle's at configs[1] by > 30 % at t = 499, err ~ 2e-7), so a stop
+    iteration there is not a property of the algorithm"""
+    rm = np.minimum.accumulate(err)
+    c = [t for t in range(lo, min(hi, len(err) - 2) + 1) if err[t] * gap <= rm[t - 1]]
+    if not c:
+        return None, None
+    t = max(c, key=lambda q: rm[q - 1] / err[q])
+    return t, float(np.sqrt(err[t] * rm[t - 1]))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["configs1", "configs2"])
+def test_stop_rule_full_size_against_oracle_trace(name):
+    """ERR_BOUND on the default one-pass path at full size (lasso.py:141-150): a bound read off the C
+    oracle's error-criterion trace of the long-horizon fixture stops the device solve at the oracle's
+    iteration exactly, graph and eager, past the first exact refresh of the carried gradient
+    (configs[1]: t = 267, a 4.5 % gap; configs[2]: t = 278, 3.1 %).  The reference-run fixtures of
+    tests/test_onepass.py pin the stop where the carried gradient is 255 iterations old.  configs[3]
+    has no such point: after iteration 256 its trace falls by less than 0.05 % per iteration."""
+    fx = dict(np.load(os.path.join(GOLD, f"longrun_{name}.npz")))
+    m, n, IT, mu = int(fx["m"]), int(fx["n"]), int(fx["iters"]), float(fx["mu"])
+    err = fx["err_iter"][:IT]
+    T, bound = stop_target(err)
+    assert T is not None
+    A = H.torch_A(m, n, "cuda:0")
+    b = H.torch_b(A)
+    gc = type("GC_float", (GPU_Calculation,), {"TYPE": "float"})(A, 1, device=0)
+    for graph in (True, False):
+        res = gc.run(b, mu, IT, err_bound=bound, record=True, use_graph=graph)
+        dev = res["err_iter"][:res["t_last"] + 1]
+        k = min(len(dev), T + 1)
+        dmax = float(np.max(np.abs(dev[:k] - err[:k]) / err[:k]))
+        assert gc.solver_stat("onepass") == 1 and gc.solver_stat("fallbacks") == 0
+        assert res["stopped"] and res["t_last"] == T, (graph, res["t_last"], T, dmax)
+        np.testing.assert_allclose(dev, err[:T + 1], rtol=1e-4, atol=1e-6 * err[0])
+    print(f"{name}: ERR_BOUND {bound:.6e} stops at t = {T} as the oracle's trace does "
+          f"(largest relative deviation of the device's trace up to t: {dmax:.2e})")
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("d_split,carry", [(1, 0), (2, 0), (1, 1)])
 def test_panel_long_horizon_against_oracle(d_split, carry):

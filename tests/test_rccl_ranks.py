@@ -144,6 +144,23 @@ def test_rccl_row_shards_collective_recovery(golden, tmp_path):
         assert rel(out[0][f"x_{tag}"], fx["x"]) <= 1e-9, (tag, rel(out[0][f"x_{tag}"], fx["x"]))
 
 
+def _one_gpu_x(fx, iters):
+    """x after `iters` iterations of the single-GPU product path on the fixture's hash instance
+    (tests/test_longrun.py holds that path to the C oracle's fixture over the whole horizon)"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import hash_instance as H
+    from convex_optimization_amd.gpu_calculation import GPU_Calculation
+    m, n = int(fx["m"]), int(fx["n"])
+    A = H.torch_A(m, n, "cuda:0")
+    b = H.torch_b(A, row0=0, m_total=m)
+    gc = type("GC_float", (GPU_Calculation,), {"TYPE": "float"})(A, 1, device=0)
+    x = gc.run(b, float(fx["mu"]), iters)["x"]
+    del gc, A, b
+    torch.cuda.empty_cache()
+    return x
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_row_shards_configs2_long_horizon(world, tmp_path):
@@ -182,20 +199,40 @@ def test_rccl_row_shards_configs2_long_horizon(world, tmp_path):
         e = rel(out[0]["x"], fx["x"])
         what = "the C oracle"
     else:
-        import sys
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import hash_instance as H
-        from convex_optimization_amd.gpu_calculation import GPU_Calculation
-        m, n = int(fx["m"]), int(fx["n"])
-        A = H.torch_A(m, n, "cuda:0")
-        b = H.torch_b(A, row0=0, m_total=m)
-        gc = type("GC_float", (GPU_Calculation,), {"TYPE": "float"})(A, 1, device=0)
-        x1 = gc.run(b, float(fx["mu"]), IT)["x"]
-        del gc, A
-        torch.cuda.empty_cache()
-        e = rel(out[0]["x"], x1)
+        e = rel(out[0]["x"], _one_gpu_x(fx, IT))
         what = "the one-GPU product path"
         assert e <= 1e-8, e
     print(f"configs2 over {world} RCCL row ranks ({int(out[0]['cus'])} CUs each, "
           f"{'one pass' if onepass else 'two passes'}), {IT} iterations: rel l2 vs {what} {e:.3e}")
+    assert e <= 1e-5, e
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,fp32", [(4, False), (4, True), (8, True)])
+def test_rccl_row_shards_configs1_long_horizon_exchange(world, fp32, tmp_path):
+    """configs[1] (8192 x 65536 fp32) over 4 and 8 RCCL row ranks on one GPU's CU partitions (2048 /
+    1024 rows per rank: 16 segment blocks, one pass), against the C oracle's fixture
+    (tests/golden/longrun_configs1.npz): with the default fp64 exchange and with the opt-in fp32 one
+    (U rounded to fp32 per rank before the cross-rank sum, the line-search scalars as hi + lo pairs;
+    half the all-reduce bytes).  World 4 runs the reference's 1000 iterations (x against the oracle);
+    world 8 the first 300 (eight processes exchange over loopback sockets at ~0.16 s per all-reduce
+    on one box: x against the single-GPU product path after the same 300 iterations).  All within
+    north_star's 1e-5 on x -- the measurement behind keeping fp64 the default."""
+    fx = dict(np.load(os.path.join(ROOT, "tests", "golden", "longrun_configs1.npz")))
+    IT = int(fx["iters"]) if world <= 4 else 300
+    extra = ["--cumask", "--iters", str(IT)] + (["--exchange-fp32"] if fp32 else [])
+    out = _launch("longrun_configs1", "rows", tmp_path, world, extra, timeout=540)
+    for o in out:
+        assert bool(o["samples_ok"]) and bool(o["b_ok"]) and int(o["iters"]) == IT
+        assert int(o["onepass"]) == 1 and int(o["fallbacks"]) == 0
+    for o in out[1:]:
+        np.testing.assert_array_equal(out[0]["x"], o["x"])
+    ref = fx["err_iter"][:IT]
+    np.testing.assert_allclose(out[0]["err"][:IT], ref, rtol=1e-3, atol=1e-6 * ref[0])
+    if IT == int(fx["iters"]):
+        e, what = rel(out[0]["x"], fx["x"]), "the C oracle"
+    else:
+        e, what = rel(out[0]["x"], _one_gpu_x(fx, IT)), "the one-GPU product path"
+    print(f"configs1 over {world} RCCL row ranks, {'fp32' if fp32 else 'fp64'} exchange, {IT} iterations: "
+          f"rel l2 vs {what} {e:.3e}")
     assert e <= 1e-5, e
