@@ -697,7 +697,7 @@ int recover_onepass(bpgl_ctx* c, DevState& st) {
 extern "C" {
 
 const char* bpgl_last_error(void) { return bpgl_host::g_err.c_str(); }
-int bpgl_version(void) { return 301; }
+int bpgl_version(void) { return 302; }
 
 int bpgl_stream_create(int device, const uint32_t* cu_mask, int32_t mask_words, void** out) {
     if (!out) return fail(BPGL_E_ARG, "out is null");

@@ -64,7 +64,10 @@ const char* bpgl_last_error(void);
  *                tuning keys "fused", "onepass_fold", "onepass_variant"; panel keys "lo8",
  *                "r_refresh", "write_through", "op_pad", "waves*", interleave 3; panel stat
  *                "refreshes"; bpgl_panel_refresh.
- *   301 (0.3.1): tuning key "onepass_rows" and solver stat "onepass_rows". */
+ *   301 (0.3.1): tuning key "onepass_rows" and solver stat "onepass_rows".
+ *   302 (0.3.2): RCCL row shards whose row needs more segment blocks than the stream's CUs run
+ *                the two-pass row iteration instead of failing at bpgl_solver_reset; the panel's
+ *                fused update is admitted against the stream's CUs; panel stat "fuse_cus". */
 int bpgl_version(void);
 
 /*
@@ -269,7 +272,11 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   over A per iteration, the gradient carried as g += gamma A^T (A D); needs
  *   one feature block, one rank (or row shards), at most
  *   128 x 4096 columns (fp32; 128 x 6144 for bf16, 128 x 2048 for fp64) and all
- *   of its blocks resident at once (nothing else running on the device).
+ *   of its blocks resident at once (nothing else running on the device): its segment
+ *   blocks per row must fit the CUs the stream may use.  When they do not (e.g. a
+ *   row of 524288 fp32 columns on a 64-CU partition), auto runs two passes; RCCL
+ *   row shards then run the two-pass row iteration (exact g through an all-reduce
+ *   of w, s23 on the local rows) -- since ABI 302; before, such a context was refused.
  *   "onepass_cache_permille" (default -1 = auto: 750 when this rank's A block is
  *   at most 320 MiB, i.e. about the 256 MiB Infinity Cache, else 0): share of every
  *   row group the one-pass kernel reads with cache-allocating loads (launches
