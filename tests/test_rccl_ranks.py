@@ -215,12 +215,16 @@ def test_rccl_row_shards_configs1_long_horizon_exchange(world, fp32, tmp_path):
     (tests/golden/longrun_configs1.npz): with the default fp64 exchange and with the opt-in fp32 one
     (U rounded to fp32 per rank before the cross-rank sum, the line-search scalars as hi + lo pairs;
     half the all-reduce bytes).  World 4 runs the reference's 1000 iterations (x against the oracle);
-    world 8 the first 300 (eight processes exchange over loopback sockets at ~0.16 s per all-reduce
-    on one box: x against the single-GPU product path after the same 300 iterations).  All within
-    north_star's 1e-5 on x -- the measurement behind keeping fp64 the default."""
+    world 8 the first 300 (x against the single-GPU product path after the same 300 iterations),
+    enqueued 8 iterations (one captured graph) at a time with the stream drained in between: eight
+    processes on ONE GPU exchanging over loopback sockets stalled when all 300 were enqueued at once
+    (profiles/r06/check_g; the bench's N > 1 legs drain every window too, and on an 8-GPU node each
+    rank has its own device).  All within north_star's 1e-5 on x -- the measurement behind keeping
+    fp64 the default."""
     fx = dict(np.load(os.path.join(ROOT, "tests", "golden", "longrun_configs1.npz")))
     IT = int(fx["iters"]) if world <= 4 else 300
-    extra = ["--cumask", "--iters", str(IT)] + (["--exchange-fp32"] if fp32 else [])
+    extra = ["--cumask", "--iters", str(IT)] + (["--exchange-fp32"] if fp32 else []) + \
+        (["--chunk", "8"] if world == 8 else [])
     out = _launch("longrun_configs1", "rows", tmp_path, world, extra, timeout=540)
     for o in out:
         assert bool(o["samples_ok"]) and bool(o["b_ok"]) and int(o["iters"]) == IT
