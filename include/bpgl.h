@@ -290,7 +290,8 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for
  *   a caller-side exchange): row shards' per-iteration exchange in fp32 -- half the
- *   bytes, x within 2e-7 (1 rank) to 1.5e-6 (8 ranks) of the fp64 exchange.
+ *   bytes, x within 2e-7 (1 rank) to 1.5e-6 (8 ranks, 120 iterations) of the fp64 exchange;
+ *   5.7e-6 from the one-GPU path after 300 iterations at 8 ranks (round 6: kept opt-in).
  *   "onepass_fail_at" (test hook, default -1): the one-pass launch of iteration t
  *   reports a row hand-off failure once (exercises the recovery above).
  *   "cus" (before bpgl_bind only; default: the stream's CU mask, else the device):
