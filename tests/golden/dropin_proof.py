@@ -43,6 +43,12 @@ def main():
     make_golden.make_case(mods, "bound_b4_p2_f32in", 99, 96, 320, 0.3, 4, 2, 2000, True, err_bound=1e-3)
     make_golden.make_case(mods, "random_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 64, True,
                           random_order=True, py_seed=5)
+    for name, (P, eb) in make_golden.STOP_CASES.items():    # round 6: the one-pass stop rule's pins
+        make_golden.make_case(mods, name, 20190327, 256, 4096, 0.4, 1, P, 600, True, err_bound=eb)
+    make_golden.make_case(mods, "randbound231_b4_p2_f32in", 1234, 128, 512, 0.4, 4, 2, 600, True,
+                          err_bound=2.5544e-4, random_order=True, py_seed=7)
+    make_golden.make_case(mods, "randbound545_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 800, True,
+                          err_bound=7.16e-6, random_order=True, py_seed=7)
     bad = []
     for name in sorted(os.listdir(out)):
         a = np.load(os.path.join(out, name))

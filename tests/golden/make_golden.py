@@ -128,6 +128,8 @@ def make_case(mods, name, seed, N, K, den, BLOCK, P, ITER_MAX, f32_inputs,
                order=res["order"], d_ATA=res["d_ATA"], A_checksum=a_checksum(A),
                err_bound=np.float64(-1.0 if err_bound is None else err_bound),
                random_order=np.bool_(random_order), stopped=np.bool_(stopped))
+    if py_seed is not None:
+        out["py_seed"] = np.int64(py_seed)   # the stdlib random seed of the shuffled order
     np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
     print(f"{name}: N={N} K={K} BLOCK={BLOCK} P={P} iters={iters} "
           f"mu={mu:.6f} |x|={np.linalg.norm(res['x']):.6f} err_last={res['err_iter'][res['t_last']]:.3e}")
@@ -199,6 +201,15 @@ def main():
         case(name, 20190327, 256, 4096, 0.4, 1, P, 600, True, err_bound=eb)
     # random block order (lasso.py:303-306), seeded stdlib random
     case("random_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 64, True, random_order=True, py_seed=5)
+    # ERR_BOUND under the shuffled order: the reference counts errors below the bound since the last
+    # update of block BLOCK - 1 and tests the count only when that block is updated (lasso.py:141-150),
+    # wherever it falls in the sweep.  At t = 231 the stop fires although block 3's own error is above
+    # the bound (four others below since its previous update); at t = 545 with it below.  Every error
+    # of either run is >= 3 % away from its bound (read off the C oracle's trace of the same order).
+    case("randbound231_b4_p2_f32in", 1234, 128, 512, 0.4, 4, 2, 600, True, err_bound=2.5544e-4,
+         random_order=True, py_seed=7)
+    case("randbound545_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 800, True, err_bound=7.16e-6,
+         random_order=True, py_seed=7)
 
 
 if __name__ == "__main__":

@@ -125,7 +125,8 @@ def test_solver_matches_reference_run(golden, case, type_name):
     assert np.all(np.diff(res["time_iter"][:T]) >= 0)
 
 
-@pytest.mark.parametrize("case", ["c1_b2_p4_f32in", "random_b4_p1_f32in", "bound_b4_p2_f32in"])
+@pytest.mark.parametrize("case", ["c1_b2_p4_f32in", "random_b4_p1_f32in", "bound_b4_p2_f32in", "stop511_b1_p1_f32in",
+                                  "stop257_b1_p4_f32in", "randbound231_b4_p2_f32in", "randbound545_b4_p1_f32in"])
 def test_drivers_on_device(golden, case):
     fx = golden(case)
     A = oracle.fixture_A(fx)
@@ -135,8 +136,9 @@ def test_drivers_on_device(golden, case):
     eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
     x = fx["x"].reshape(-1)
     import random
+    py_seed = int(fx.get("py_seed", 5))
     for cls in ((lasso.ClassLassoR,) if bool(fx["random_order"]) else (lasso.ClassLasso, lasso.ClassLassoDevice)):
-        random.seed(5)
+        random.seed(py_seed)
         drv = cls(gc, d, A, fx["b"], float(fx["mu"]), BLOCK, IT)
         err_iter = np.zeros(IT)
         drv.run(ERR_BOUND=eb, err_iter=err_iter, SILENCE=True)
@@ -148,9 +150,10 @@ def test_drivers_on_device(golden, case):
                 lasso.ClassLassoDevice.__init__(self, *a)
                 self.idx_shuffle = np.arange(self.BLOCK)
             index_get = lasso.ClassLassoR.index_get
-        random.seed(5)
+        random.seed(py_seed)
         drv = DevR(gc, d, A, fx["b"], float(fx["mu"]), BLOCK, IT)
-        drv.run(SILENCE=True)
+        drv.run(ERR_BOUND=eb, SILENCE=True)
+        assert drv.iters == int(fx["t_last"]) + 1
         assert rel(drv.x, x) <= 1e-9
 
 

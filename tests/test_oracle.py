@@ -17,6 +17,10 @@ X_TOL = 1e-9
 
 def _run_args(fx):
     order = fx["order"] if bool(fx["random_order"]) else None
+    if order is not None and len(order) < int(fx["ITER_MAX"]):
+        # a run that stopped early captured only the blocks it updated; the padding (the last block,
+        # as the device reads a short order) is never reached when the stop is reproduced
+        order = np.concatenate([order, np.full(int(fx["ITER_MAX"]) - len(order), order[-1], dtype=order.dtype)])
     eb = None if fx["err_bound"] < 0 else float(fx["err_bound"])
     return order, eb
 
