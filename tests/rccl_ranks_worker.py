@@ -82,7 +82,8 @@ def main():
         # every rank's set-up is finished before any rank's solve starts (nothing else on the GPU)
         torch.cuda.synchronize()
         dist.barrier()
-        res = gc.run(b_local, float(fx["mu"]), iters, err_bound=eb, record=True, use_graph=graph)
+        order = fx["order"] if bool(fx["random_order"]) else None   # the reference's shuffled block order
+        res = gc.run(b_local, float(fx["mu"]), iters, err_bound=eb, order=order, record=True, use_graph=graph)
         tag = "graph" if graph else "eager"
         out[f"x_{tag}"] = np.asarray(res["x"]).reshape(-1)
         out[f"err_{tag}"] = np.asarray(res["err_iter"])
