@@ -576,7 +576,7 @@ __device__ __forceinline__ void panel_norms_out(const PanelParams& p, const doub
     }
 }
 
-// BPGL_PANEL_DIAG (timing-only builds, tools/panel_epi_diag.sh; results wrong): bit 0 -- no carried-G
+// BPGL_PANEL_DIAG (timing-only builds, tools/panel_diag.sh; results wrong): bit 0 -- no carried-G
 // store, bit 1 -- no D' store, bit 3 -- no epilogue loop at all (the products are only kept alive)
 template <int NTW, int EPI, int DS, int GM = 0, int NW = 0>
 __device__ __forceinline__ void panel_pass1_epilogue(const PanelParams& p, int mb, long long c0, int wm, int wn,

@@ -44,7 +44,7 @@ def durations(d):
 def main():
     root = sys.argv[1]
     dur = durations(os.path.join(root, "trace"))
-    res = {"source": os.environ.get("MFMA_SOURCE", "tools/profile_r04b.sh (rocprofv3 --pmc, one pass per k; round 4 defaults: d_split 1, carried gradient) + kernel trace of bench.py --config 4"),
+    res = {"source": os.environ.get("MFMA_SOURCE", "tools/profile.sh (rocprofv3 --pmc, one pass per k) + kernel trace of bench.py --config 4"),
            "simds": SIMDS, "peak_clock_hz": PEAK_HZ}
     for kdir in sorted(glob.glob(os.path.join(root, "k*"))):
         k = os.path.basename(kdir)
