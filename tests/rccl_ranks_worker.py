@@ -7,7 +7,7 @@ The data path is the product's: libbpgl's communicator, the all-reduce issued on
 stream.
 
 usage: rccl_ranks_worker.py CASE SHARD OUTDIR [--cumask] [--fail-rank R --fail-at T] [--iters N]
-                           [--exchange-fp32] [--chunk N]
+                           [--exchange-fp32] [--chunk N] [--eager]
   CASE: a reference fixture of tests/golden, or longrun_<config> (a full-size long-horizon fixture,
         row shards only: see longrun())
   SHARD: columns | rows
@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--iters", type=int, default=0, help="longrun: iterations (0: the fixture's own)")
     ap.add_argument("--exchange-fp32", action="store_true", help="longrun: the opt-in fp32 exchange (tuning -1)")
     ap.add_argument("--chunk", type=int, default=0, help="longrun: enqueue this many iterations at a time (0: all)")
+    ap.add_argument("--eager", action="store_true", help="longrun: eager launches instead of hipGraph replay")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ["NCCL_HOSTID"] = f"bpgl-test-rank{rank}"   # before the communicator is created
@@ -128,19 +129,10 @@ def longrun(a, fx, rank, world, np, torch, dist, D, GPU_Calculation):
         gc.set_tuning("exchange_fp32", -1)
     torch.cuda.synchronize()
     dist.barrier()
-    if os.environ.get("BPGL_WORKER_PROGRESS"):   # diagnostics: the same solve in 25-iteration steps
-        import time
-        t0 = time.time()
-        gc.solver_reset(b, mu, record_len=iters, use_graph=True)
-        for k in range(0, iters, 25):
-            gc.solver_step(min(25, iters - k))
-            gc.stream.synchronize()
-            if rank == 0:
-                print(f"rank 0: {min(k + 25, iters)} iterations, {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     if a.chunk:
         # the solve enqueued `chunk` iterations at a time, the stream drained in between (see the world-8
         # case of test_rccl_row_shards_configs1_long_horizon_exchange)
-        gc.solver_reset(b, mu, record_len=iters, use_graph=not os.environ.get("BPGL_WORKER_EAGER"))
+        gc.solver_reset(b, mu, record_len=iters, use_graph=not a.eager)
         for k in range(0, iters, a.chunk):
             gc.solver_step(min(a.chunk, iters - k))
             gc.stream.synchronize()
@@ -148,7 +140,7 @@ def longrun(a, fx, rank, world, np, torch, dist, D, GPU_Calculation):
         res["x"] = gc.solver_x()
         res["err_iter"], _ = gc.solver_records()
     else:
-        res = gc.run(b, mu, iters, record=True, use_graph=not os.environ.get("BPGL_WORKER_EAGER"))
+        res = gc.run(b, mu, iters, record=True, use_graph=not a.eager)
     out = {"x": np.asarray(res["x"]).reshape(-1), "err": np.asarray(res["err_iter"]),
            "iters": np.int64(res["iters"]), "samples_ok": np.bool_(samples_ok), "b_ok": np.bool_(b_ok),
            "in_place": np.bool_(gc._A_dev.data_ptr() == A.data_ptr()),
