@@ -140,6 +140,8 @@ def parse():
                     help="permille of each one-pass row group read with cache-allocating loads (-1: library default)")
     ap.add_argument("--onepass-rows", type=int, default=-1, choices=[-1, 0, 1],
                     help="one-pass row groups: 1 interleaved rows, 0 consecutive (-1: library default)")
+    ap.add_argument("--onepass-sb1", type=int, default=-1, choices=[-1, 0],
+                    help="one segment block per row: the LDS-only row hand-off (-1: library default, on) or off (0)")
     ap.add_argument("--comm", action="store_true",
                     help="attach an RCCL communicator even at N = 1 (runs the sharded/all-reduce leg)")
     ap.add_argument("--shard", default="auto", choices=["auto", "rows", "columns"],
@@ -357,6 +359,8 @@ def measure(ctx, args, m, n_total):
         gc.set_tuning("onepass_cache_permille", args.onepass_cache)
     if args.onepass_rows >= 0:
         gc.set_tuning("onepass_rows", args.onepass_rows)
+    if args.onepass_sb1 >= 0:
+        gc.set_tuning("onepass_sb1", args.onepass_sb1)
     if args.graph_max > 0:
         gc.set_tuning("graph_max", args.graph_max)
 

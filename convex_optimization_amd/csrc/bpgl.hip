@@ -96,6 +96,7 @@ struct bpgl_ctx {
     // permille of each row group read with cache-allocating loads (-1: auto, op_cache_auto)
     int op_cache = -1;
     int op_rows = -1;          // tuning "onepass_rows": -1 auto, 0 consecutive, 1 interleaved
+    int op_sb1 = -1;           // tuning "onepass_sb1": -1 auto (on when SB = 1), 0 off
     bool op_shape = false;     // the shape admits it (geometry)
     bool op_on = false;        // this solver run uses it
     int op_SB = 0, op_ngroups = 0, op_R = 0, op_xl = 0, op_tail_grid = 0, op_gpl = 1;
@@ -186,8 +187,11 @@ int op_cache_eff(const bpgl_ctx* c) {
 // strong shard, 63.0 / 62.7 us on one box, 51.6 -> 52.9 us on another), with one segment block per row
 // (configs[3], 2709 -> 2757 us) and at 2 groups (the weak shard, 328 -> 333.7 us); profiles/r05/layout,
 // profiles/r05/rows.  Results agree to rounding (the U partials sum other rows per group).
+// granules per lane of the k_onepass instantiation in use: 0 = one segment block per row with the
+// LDS-only hand-off ("onepass_sb1", default on when SB = 1; round 6), else 1 (SB <= 64) or 2
+int op_gpl_eff(const bpgl_ctx* c) { return (c->op_SB == 1 && c->op_sb1 != 0) ? 0 : c->op_gpl; }
 int op_rows_eff(const bpgl_ctx* c) {
-    if (c->op_gpl == 2) return 0;   // the interleaved kernel is instantiated for SB <= 64 only
+    if (op_gpl_eff(c) != 1) return 0;   // the interleaved kernel is instantiated for 1 < SB <= 64 only
     if (c->op_rows >= 0) return c->op_rows;
     return c->op_SB >= 16 && c->op_ngroups >= 8 && c->op_R >= 128 ? 1 : 0;
 }
@@ -321,7 +325,8 @@ template <typename T, int GPL, bool RILV>
 const void* onepass_fn_g() { return (const void*)k_onepass<T, OpRing<T>::NB, OpRing<T>::PF, OpLU<T>::LU, GPL, RILV>; }
 template <typename T>
 const void* onepass_fn_t(int gpl, int rilv) {
-    return gpl == 2 ? onepass_fn_g<T, 2, false>() : rilv ? onepass_fn_g<T, 1, true>() : onepass_fn_g<T, 1, false>();
+    return gpl == 2 ? onepass_fn_g<T, 2, false>() : gpl == 0 ? onepass_fn_g<T, 0, false>()
+                     : rilv ? onepass_fn_g<T, 1, true>() : onepass_fn_g<T, 1, false>();
 }
 const void* onepass_fn(int dtype, int gpl, int rilv) {
     return dtype == BPGL_F32 ? onepass_fn_t<float>(gpl, rilv) : dtype == BPGL_F64 ? onepass_fn_t<double>(gpl, rilv)
@@ -334,7 +339,9 @@ void onepass_launch_g(bpgl_ctx* c) {
 }
 template <typename T>
 void onepass_launch_t(bpgl_ctx* c) {
-    if (c->op_gpl == 2) onepass_launch_g<T, 2, false>(c);
+    const int gpl = op_gpl_eff(c);
+    if (gpl == 2) onepass_launch_g<T, 2, false>(c);
+    else if (gpl == 0) onepass_launch_g<T, 0, false>(c);
     else if (c->op.rilv) onepass_launch_g<T, 1, true>(c);
     else onepass_launch_g<T, 1, false>(c);
 }
@@ -406,7 +413,7 @@ const char* onepass_ineligible(bpgl_ctx* c) {
     if (!c->rows && (c->nranks != 1 || c->comm || c->external))
         return "column shards need a single rank without a communicator (row shards run it on several)";
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, c->op_gpl, op_rows_eff(c)), kThreads, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, onepass_fn(c->dtype, op_gpl_eff(c), op_rows_eff(c)), kThreads, 0) != hipSuccess || nb < 1)
         return "kernel does not fit on a CU";
     if ((int64_t)c->op_ngroups * c->op_SB > (int64_t)nb * c->cus) return "grid exceeds the resident capacity";
     return nullptr;
@@ -1126,6 +1133,7 @@ int bpgl_solver_stat(bpgl_ctx* c, const char* key, int64_t* value) {
     else if (!strcmp(key, "cu_masked")) *value = c->cu_masked ? 1 : 0;
     else if (!strcmp(key, "onepass_grid")) *value = (int64_t)c->op_ngroups * c->op_SB;
     else if (!strcmp(key, "onepass_rows")) *value = c->op_shape ? op_rows_eff(c) : 0;
+    else if (!strcmp(key, "onepass_sb1")) *value = c->op_shape && op_gpl_eff(c) == 0 ? 1 : 0;
     else return fail(BPGL_E_ARG, "unknown stat '%s'", key);
     return 0;
 }
@@ -1194,6 +1202,14 @@ int bpgl_set_tuning(bpgl_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "onepass_rows")) {
         if (value < -1 || value > 1) return fail(BPGL_E_ARG, "onepass_rows must be -1 (auto), 0 or 1");
         c->op_rows = (int)value;
+        if (c->op_shape) c->op.rilv = op_rows_eff(c);
+        drop_graphs(c);
+        c->solver = false;
+        return 0;
+    }
+    if (!strcmp(key, "onepass_sb1")) {
+        if (value < -1 || value > 0) return fail(BPGL_E_ARG, "onepass_sb1 must be -1 (auto) or 0");
+        c->op_sb1 = (int)value;
         if (c->op_shape) c->op.rilv = op_rows_eff(c);
         drop_graphs(c);
         c->solver = false;

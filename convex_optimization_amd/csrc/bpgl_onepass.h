@@ -262,12 +262,16 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             u[k][e] = 0.0;
         }
     }
-    static_assert(GPL == 1 || GPL == 2, "granules per lane");
-    int glane[GPL];   // granule k of this lane: segment block lane + 64 k
+    // GPL 0: one segment block per row (SB = 1, e.g. configs[3]): a row's s23 is complete inside the
+    // block, so phase 2 folds the 4 wave partials straight from the LDS slots -- no granule through
+    // memory, no publication step ("onepass_sb1", default on when SB = 1)
+    static_assert(GPL == 0 || GPL == 1 || GPL == 2, "granules per lane");
+    constexpr int NG = GPL > 0 ? GPL : 1;
+    int glane[NG];   // granule k of this lane: segment block lane + 64 k
 #pragma unroll
-    for (int k = 0; k < GPL; ++k) glane[k] = lane + 64 * k < SB ? lane + 64 * k : 0;
+    for (int k = 0; k < NG; ++k) glane[k] = lane + 64 * k < SB ? lane + 64 * k : 0;
     raw buf[NB][LU];
-    op_u64 gv[NB][GPL];
+    op_u64 gv[NB][NG];
     unsigned polls = kOpPolls;
     bool failed = o.fail_at >= 0 && b == 0 && p.st->t == o.fail_at;   // test hook (bpgl_set_tuning)
 
@@ -281,6 +285,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
         for (int k = 0; k < LU; ++k) buf[slot][k] = ldv<T, decltype(NTL)::value>(rp + col[k]);
     };
     auto gload = [&](int t, int slot) {   // granules consumed at step t (phase 2 of row t - LAG)
+        if constexpr (GPL == 0) return;
         int t2 = t - LAG;
         t2 = t2 < 0 ? 0 : (t2 >= nrows ? nrows - 1 : t2);
 #pragma unroll
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         const int tp = t - kOpDelta;   // publication of row tp by wave tp % 4
-        if (tp >= 0 && tp < nrows && (tp & 3) == wave) {
+        if (GPL > 0 && tp >= 0 && tp < nrows && (tp & 3) == wave) {
             const unsigned want = ((unsigned)tp >> kOpSlotsLog) & 1u;
             op_u64 w = 0;
             while (true) {
@@ -333,9 +338,32 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
         const int t2 = t - LAG;
-        if (t2 >= 0 && t2 < nrows) {   // phase 2: U += row(t2) * s23[t2]
+        if (GPL == 0 && t2 >= 0 && t2 < nrows) {   // phase 2, one segment block: s23[t2] from the LDS slots
             const int qs = (q - LAG + NB) % NB;
-            op_u64 v[GPL];
+            const unsigned want = ((unsigned)t2 >> kOpSlotsLog) & 1u;
+            op_u64 w = 0;
+            while (true) {   // every wave wrote its partial of row t2 at its step t2 (LAG steps ago: rarely late)
+                w = lane < kWaves ? __hip_atomic_load(&part[t2 % kOpSlots][lane], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP)
+                                  : 0;
+                if (__all(lane >= kWaves || op_tag(w) == want)) break;
+                if (polls == 0) { failed = true; break; }
+                --polls;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            const double x = op_lane(op_quad_sum(op_unstuff(w)), 0);   // (p0 + p1) + (p2 + p3)
+            if (wave == 0 && lane == 0) o.S[rowof(t2)] = x;
+#pragma unroll
+            for (int k = 0; k < LU; ++k) {
+                double v2[N];
+                VecT<T>::cvt(buf[qs][k], v2);
+#pragma unroll
+                for (int e = 0; e < N; ++e) u[k][e] = fma(v2[e], x, u[k][e]);
+            }
+        }
+        if (GPL > 0 && t2 >= 0 && t2 < nrows) {   // phase 2: U += row(t2) * s23[t2]
+            const int qs = (q - LAG + NB) % NB;
+            op_u64 v[NG];
 #pragma unroll
             for (int k = 0; k < GPL; ++k) v[k] = gv[q][k];
             // lanes past SB read block 0's granule (glane), which is ready exactly when block 0's is:
@@ -343,7 +371,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
             auto ready = [&]() {
                 bool ok = true;
 #pragma unroll
-                for (int k = 0; k < GPL; ++k) ok = ok && op_tag(v[k]) == tag;
+                for (int k = 0; k < NG; ++k) ok = ok && op_tag(v[k]) == tag;
                 return ok;
             };
             if (!__all(ready())) {   // late: re-poll (drains this wave's queue; rare)
@@ -353,17 +381,17 @@ __global__ __launch_bounds__(kThreads, 1) void k_onepass(Params p, OnePassArgs o
                     --polls;
                     __builtin_amdgcn_s_sleep(2);
 #pragma unroll
-                    for (int k = 0; k < GPL; ++k)
+                    for (int k = 0; k < NG; ++k)
                         v[k] = __hip_atomic_load(src + glane[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 } while (!__all(ready()));
                 // settle here, so the merge with the fast path is not a pending load
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-                for (int k = 0; k < GPL; ++k) asm volatile("" : "+v"(v[k]));
+                for (int k = 0; k < NG; ++k) asm volatile("" : "+v"(v[k]));
             }
             // GPL 2 means SB > 64: every lane's first granule is a block of its own
             double x = (GPL == 2 || lane < SB) ? op_unstuff(v[0]) : 0.0;
-            if (GPL == 2) x += lane + 64 < SB ? op_unstuff(v[GPL - 1]) : 0.0;   // blocks l and l + 64, then the wave
+            if (GPL == 2) x += lane + 64 < SB ? op_unstuff(v[NG - 1]) : 0.0;   // blocks l and l + 64, then the wave
             x = SB <= 16 ? op_lane(op_row_sum16(x), 0) : op_wave_sum(x);
             if (sb == 0 && wave == 0 && lane == 0) o.S[rowof(t2)] = x;
 #pragma unroll

@@ -67,7 +67,8 @@ const char* bpgl_last_error(void);
  *   301 (0.3.1): tuning key "onepass_rows" and solver stat "onepass_rows".
  *   302 (0.3.2): RCCL row shards whose row needs more segment blocks than the stream's CUs run
  *                the two-pass row iteration instead of failing at bpgl_solver_reset; the panel's
- *                fused update is admitted against the stream's CUs; panel stat "fuse_cus". */
+ *                fused update is admitted against the stream's CUs; panel stat "fuse_cus"; tuning
+ *                key and solver stat "onepass_sb1". */
 int bpgl_version(void);
 
 /*
@@ -286,6 +287,10 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   group g of the one-pass kernel owns rows g, g + ngroups, ... (the groups read
  *   adjacent rows at once; with at most 64 segment blocks per row, else always 0),
  *   0 = R consecutive rows; bpgl_solver_stat("onepass_rows") reports the form in use.
+ *   "onepass_sb1" (default -1 = on when a row is one segment block, 0 = off): with one
+ *   segment block per row (e.g. 4096 fp32 columns) the row's s23 is folded from the 4 wave
+ *   partials in LDS instead of a tagged granule through memory (configs[3] +2 %; results agree
+ *   with the granule path to its parity bit); bpgl_solver_stat("onepass_sb1") reports it.
  *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for

@@ -160,6 +160,36 @@ def test_interleaved_row_groups(m, n, type_name):
         gc.set_tuning("onepass_rows", 2)
 
 
+@pytest.mark.parametrize("m,n,type_name", [(4099, 1536, "float"), (40000, 4096, "float"), (3, 5, "float"),
+                                            (2000, 1000, "double"), (1500, 6000, "bf16")])
+def test_one_segment_block_lds_hand_off(m, n, type_name):
+    """One segment block per row (configs[3]'s shape class): phase 2 folds the row's 4 wave partials
+    straight from LDS ("onepass_sb1", the default there) instead of a tagged granule through memory.
+    Against the granule path: the same algorithm and the same fold order, the granule's parity bit
+    aside (<= 1 ulp per row): <= 1e-12 after 5 iterations, <= 1e-8 after 25, the same stop iteration;
+    graph = eager bitwise; the stat reports the path in use"""
+    rs = np.random.RandomState(m + n)
+    A = rs.randn(m, n) / np.sqrt(n)
+    b = A @ np.where(rs.rand(n) < 0.3, rs.randn(n), 0.0) + 0.01 * rs.randn(m)
+    mu = 0.1 * np.abs(A.T @ b).max()
+    gc = make_cls(type_name)(A, 1, device=0)
+    assert used_onepass(gc, b, mu)
+    out = {}
+    for sb1 in (-1, 0):
+        gc.set_tuning("onepass_sb1", sb1)
+        r5 = gc.run(b, mu, 5)
+        assert gc.solver_stat("onepass_sb1") == (1 if sb1 else 0)
+        g = gc.run(b, mu, 25, err_bound=1e-9, record=True, use_graph=True)
+        e = gc.run(b, mu, 25, err_bound=1e-9, record=True, use_graph=False)
+        np.testing.assert_array_equal(g["x"], e["x"])
+        out[sb1] = (r5, g)
+    assert rel(out[-1][0]["x"], out[0][0]["x"]) <= 1e-12, rel(out[-1][0]["x"], out[0][0]["x"])
+    assert rel(out[-1][1]["x"], out[0][1]["x"]) <= 1e-8, rel(out[-1][1]["x"], out[0][1]["x"])
+    assert out[-1][1]["t_last"] == out[0][1]["t_last"]
+    with pytest.raises(N.BpglError):
+        gc.set_tuning("onepass_sb1", 1)
+
+
 def test_graph_eager_split_steps_bitwise():
     rs = np.random.RandomState(5)
     A = rs.randn(900, 5000)
