@@ -188,8 +188,11 @@ int op_cache_eff(const bpgl_ctx* c) {
 // (configs[3], 2709 -> 2757 us) and at 2 groups (the weak shard, 328 -> 333.7 us); profiles/r05/layout,
 // profiles/r05/rows.  Results agree to rounding (the U partials sum other rows per group).
 // granules per lane of the k_onepass instantiation in use: 0 = one segment block per row with the
-// LDS-only hand-off ("onepass_sb1", default on when SB = 1; round 6), else 1 (SB <= 64) or 2
-int op_gpl_eff(const bpgl_ctx* c) { return (c->op_SB == 1 && c->op_sb1 != 0) ? 0 : c->op_gpl; }
+// LDS-only hand-off ("onepass_sb1", default on when SB = 1; round 6; an explicit "onepass_rows" = 1
+// takes the granule path, whose instantiation has the interleaved form), else 1 (SB <= 64) or 2
+int op_gpl_eff(const bpgl_ctx* c) {
+    return (c->op_SB == 1 && c->op_sb1 != 0 && c->op_rows != 1) ? 0 : c->op_gpl;
+}
 int op_rows_eff(const bpgl_ctx* c) {
     if (op_gpl_eff(c) != 1) return 0;   // the interleaved kernel is instantiated for 1 < SB <= 64 only
     if (c->op_rows >= 0) return c->op_rows;

@@ -290,7 +290,8 @@ int bpgl_kernel_times(bpgl_ctx* ctx, double* avg_ms /* 9 */, int64_t* samples);
  *   "onepass_sb1" (default -1 = on when a row is one segment block, 0 = off): with one
  *   segment block per row (e.g. 4096 fp32 columns) the row's s23 is folded from the 4 wave
  *   partials in LDS instead of a tagged granule through memory (configs[3] +2 %; results agree
- *   with the granule path to its parity bit); bpgl_solver_stat("onepass_sb1") reports it.
+ *   with the granule path to its parity bit; an explicit "onepass_rows" = 1 selects the
+ *   granule path); bpgl_solver_stat("onepass_sb1") reports it.
  *   "onepass_refresh" (default 256; 0 = only at reset): recompute g = A^T r
  *   exactly every this many iterations (bounds the recurrence's drift).
  *   "exchange_fp32" (default 0 = never, -1 = with an RCCL communicator, 1 = also for
