@@ -45,6 +45,7 @@ def main():
                           random_order=True, py_seed=5)
     for name, (P, eb) in make_golden.STOP_CASES.items():    # round 6: the one-pass stop rule's pins
         make_golden.make_case(mods, name, 20190327, 256, 4096, 0.4, 1, P, 600, True, err_bound=eb)
+    make_golden.make_case(mods, "raggedbound74_b3_p2_f32in", 4242, 77, 120, 0.4, 3, 2, 200, True, err_bound=8.909e-05)
     make_golden.make_case(mods, "randbound231_b4_p2_f32in", 1234, 128, 512, 0.4, 4, 2, 600, True,
                           err_bound=2.5544e-4, random_order=True, py_seed=7)
     make_golden.make_case(mods, "randbound545_b4_p1_f32in", 1234, 128, 512, 0.4, 4, 1, 800, True,

@@ -197,6 +197,8 @@ def main():
     case("ragged_b3_p2_f32in", 4242, 77, 120, 0.4, 3, 2, 60, True)
     # ERR_BOUND stopping (lasso.py:141-150)
     case("bound_b4_p2_f32in", 99, 96, 320, 0.3, 4, 2, 2000, True, err_bound=1e-3)
+    # ... on the ragged shape (every error of the run >= 13 % from the bound; round 6)
+    case("raggedbound74_b3_p2_f32in", 4242, 77, 120, 0.4, 3, 2, 200, True, err_bound=8.909e-05)
     for name, (P, eb) in STOP_CASES.items():
         case(name, 20190327, 256, 4096, 0.4, 1, P, 600, True, err_bound=eb)
     # random block order (lasso.py:303-306), seeded stdlib random

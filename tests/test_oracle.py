@@ -114,7 +114,7 @@ def test_dropin_run_of_reference_driver_is_bitwise():
     import numpy as np
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     names = sorted(f for f in os.listdir(os.path.join(here, "dropin")) if f.endswith(".npz"))
-    # every reference-run case (rounds 1-5: 7; round 6: + 3 one-pass stop pins + 2 shuffled-order stops)
+    # every reference-run case (rounds 1-5: 7; round 6: + 3 one-pass stop pins, 2 shuffled-order stops, a ragged stop)
     assert names == sorted(c + ".npz" for c in golden_cases())
     for name in names:
         a = np.load(os.path.join(here, "dropin", name))

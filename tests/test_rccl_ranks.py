@@ -54,7 +54,7 @@ def rel(a, b):
 
 @pytest.mark.parametrize("case,world", [("c1_b2_p4_f32in", 2), ("bound_b4_p2_f32in", 2), ("c1_b2_p4_f32in", 4),
                                         ("c1_b2_p4_f32in", 8), ("randbound231_b4_p2_f32in", 2),
-                                        ("randbound545_b4_p1_f32in", 4)])
+                                        ("randbound545_b4_p1_f32in", 4), ("raggedbound74_b3_p2_f32in", 2)])
 def test_two_rccl_ranks_column_shards(golden, case, world, tmp_path):
     from convex_optimization_amd import distributed as D
     fx = golden(case)
