@@ -298,7 +298,7 @@ class GPU_Calculation:
     def solver_stat(self, key):
         """Counter since the last reset (include/bpgl.h bpgl_solver_stat): "onepass", "refreshes",
         "fallbacks", "requested", "enqueued", "refresh_period", "cus", "cu_masked", "onepass_grid",
-        "onepass_rows"."""
+        "onepass_rows", "onepass_sb1"."""
         v = ctypes.c_int64()
         N.check(N.lib().bpgl_solver_stat(self._ctx, key.encode(), ctypes.byref(v)), "bpgl_solver_stat")
         return v.value
